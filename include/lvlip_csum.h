@@ -1,0 +1,176 @@
+/*
+ * lvlip_csum.h — C-ABI of the MI355X Internet-checksum offload for level-ip.
+ *
+ * This is the drop-in boundary between level-ip's C stack and the gfx950 HIP
+ * kernels in level-ip_amd/csrc/.  Every entry point is plain C: pointers,
+ * sizes and integers, no HIP or torch types.  Citations are to the reference
+ * tree (saminiir/level-ip v1) as path:line.
+ *
+ *  Group 1 — per-call drop-in (CPU, reentrant, no shared state).
+ *    Same names, signatures and results as include/utils.h:13-14
+ *    (src/utils.c:22-55).  The stack keeps calling these from
+ *    src/ip_input.c:38, src/ip_output.c:10, src/icmpv4.c:47, src/tcp.c:97.
+ *
+ *  Group 2 — batched checksum over packet descriptors on the GPU.
+ *    out[i] == checksum(base + d[i].offset, d[i].len, (int)d[i].start_sum)
+ *    bit for bit, including the reference's u32 wrap-around of the seed
+ *    (src/utils.c:46-48, src/tcp.c:92-97).
+ *
+ *  Group 3 — host-resident batches through a per-thread context (pinned
+ *    staging arena + HIP stream): gathers skb bytes, H2D, kernel, D2H.
+ *
+ * Error convention: 0 = success, negative LVLIP_E* on failure.  A batch call
+ * that fails writes nothing meaningful to out[] and never substitutes a CPU
+ * result: the caller decides what to do.
+ */
+#ifndef LVLIP_CSUM_H
+#define LVLIP_CSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* The library is built with -fvisibility=hidden: exactly the entry points
+ * declared in this header are exported. */
+#pragma GCC visibility push(default)
+
+#define LVLIP_CSUM_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------- */
+#define LVLIP_OK              0
+#define LVLIP_EINVAL         -1  /* bad argument (NULL, n too large, ...)   */
+#define LVLIP_ENODEV         -2  /* no HIP device / device index invalid     */
+#define LVLIP_EHIP           -3  /* a HIP runtime call failed                */
+#define LVLIP_ENOMEM         -4  /* device or pinned allocation failed       */
+#define LVLIP_ERANGE         -5  /* batch does not fit the context's arena   */
+
+/* ======================================================================= */
+/* Group 1: per-call drop-in, replaces src/utils.c:22-55                    */
+/* ======================================================================= */
+
+/* Replaces sum_every_16bits, src/utils.c:22-38 (decl include/utils.h:13).
+ * Sum of count/2 native little-endian u16 words, modulo 2^32, plus the odd
+ * trailing byte zero-extended; count <= 0 gives 0. */
+uint32_t sum_every_16bits(void *addr, int count);
+
+/* Replaces checksum, src/utils.c:40-55 (decl include/utils.h:14).
+ * T = (uint32_t)start_sum + sum_every_16bits(addr, count) (mod 2^32), folded
+ * with while (T >> 16) T = (T & 0xffff) + (T >> 16), returned as (uint16_t)~T.
+ * The result is stored raw (no htons) by every caller. */
+uint16_t checksum(void *addr, int count, int start_sum);
+
+/* Seed arithmetic of tcp_udp_checksum, src/tcp.c:87-96: saddr + daddr +
+ * htons(proto) + htons(len), all as u32 with plain wrap-around (the carry out
+ * of bit 31 is lost, exactly as the reference loses it).  saddr/daddr are
+ * network-order words as passed at src/tcp_output.c:126. */
+uint32_t lvlip_pseudo_sum(uint32_t saddr, uint32_t daddr, uint8_t proto,
+                          uint16_t len);
+
+/* ======================================================================= */
+/* Group 2: device-resident batches                                         */
+/* ======================================================================= */
+
+/* One packet (or header) to checksum.  16 bytes, naturally aligned.
+ *   offset    byte offset of the first byte from the batch base pointer
+ *   len       byte count (the reference's `int count`); <= 0 means empty
+ *   start_sum the `int start_sum` seed, as its u32 bit pattern:
+ *             0 for IPv4 headers (src/ip_input.c:38, src/ip_output.c:10)
+ *             and ICMP (src/icmpv4.c:47); lvlip_pseudo_sum(...) for TCP
+ *             (src/tcp.c:97). */
+typedef struct lvlip_csum_desc {
+    uint64_t offset;
+    int32_t  len;
+    uint32_t start_sum;
+} lvlip_csum_desc;
+
+/* Largest batch one call accepts (packet indices are 32-bit on the GPU). */
+#define LVLIP_MAX_BATCH 0xFFFFFFF0u
+
+/* Checksums n descriptors whose bytes, descriptors and outputs are all in
+ * device memory of the current HIP device.  Asynchronous on `stream` (a
+ * hipStream_t passed as void*, NULL = the null stream).
+ *
+ * Contract on base: 16-byte aligned, and readable from base up to
+ * round_up(max(offset + len), 16): the kernel reads whole 16-byte chunks and
+ * masks the bytes outside each packet.  Any byte alignment of offset is
+ * accepted (odd offsets included).  out[i] is a raw u16 (no byte swap). */
+int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
+                         uint32_t n, uint16_t *out, void *stream);
+
+/* Kernel selection for lvlip_csum_batch_dev_ex (benchmarks, A/B tests). */
+#define LVLIP_KERNEL_AUTO      0  /* the default (kernel choice)   */
+#define LVLIP_KERNEL_WAVE      1  /* one wavefront per packet, VGPR staging       */
+#define LVLIP_KERNEL_WAVE_LDS  2  /* one wavefront per packet, LDS-DMA staging    */
+#define LVLIP_KERNEL_FLAT      3  /* chunk-balanced tile sweep (ragged batches)   */
+
+typedef struct lvlip_launch_cfg {
+    int32_t  kernel;        /* LVLIP_KERNEL_*                               */
+    int32_t  unroll;        /* 16-B loads in flight per lane (0 = default)  */
+    int32_t  waves_per_cu;  /* grid size knob, 0 = one wave per packet      */
+    int32_t  reserved;      /* must be 0                                    */
+} lvlip_launch_cfg;
+
+int lvlip_csum_batch_dev_ex(const void *base, const lvlip_csum_desc *descs,
+                            uint32_t n, uint16_t *out, void *stream,
+                            const lvlip_launch_cfg *cfg);
+
+/* ======================================================================= */
+/* Group 3: host-resident batches (per-thread context)                      */
+/* ======================================================================= */
+
+/* One host packet: the bytes a reference call site would pass to
+ * checksum(ptr, len, start_sum).  ptr may be any address (skb->head + 14 /
+ * + 34 are 2 mod 4, include/ip.h:47-50, include/tcp.h:224-227). */
+typedef struct lvlip_csum_iov {
+    const void *ptr;
+    int32_t     len;
+    uint32_t    start_sum;
+} lvlip_csum_iov;
+
+typedef struct lvlip_csum_ctx lvlip_csum_ctx;
+
+/* Creates a context on HIP device `device` with a pinned host arena and a
+ * device arena of `arena_bytes` each (0 = 64 MiB), and its own stream.
+ * A context is owned by one thread at a time (src/main.c:83-89 runs the
+ * checksum from several threads: give each its own context). */
+int lvlip_csum_ctx_create(lvlip_csum_ctx **out, int device,
+                          size_t arena_bytes);
+int lvlip_csum_ctx_destroy(lvlip_csum_ctx *ctx);
+
+/* Gathers the n host packets into the pinned arena (each at a 16-B aligned
+ * slot), copies to the device, runs the kernel, copies the n results back
+ * and waits.  Batches larger than the arena are processed in arena-sized
+ * pieces, double-buffered so the copy of one piece overlaps the kernel of
+ * the previous one.  out is host memory. */
+int lvlip_csum_batch_host(lvlip_csum_ctx *ctx, const lvlip_csum_iov *pkts,
+                          uint32_t n, uint16_t *out);
+
+/* Same, for packets already laid out in one host buffer (descriptor
+ * offsets relative to `base`, which must hold round_up(max end,16) bytes). */
+int lvlip_csum_batch_host_flat(lvlip_csum_ctx *ctx, const void *base,
+                               size_t base_bytes, const lvlip_csum_desc *d,
+                               uint32_t n, uint16_t *out);
+
+/* ======================================================================= */
+/* Misc                                                                     */
+/* ======================================================================= */
+const char *lvlip_strerror(int err);
+int lvlip_abi_version(void);
+/* Number of visible HIP devices (0 when none). */
+int lvlip_device_count(void);
+/* Last HIP error string recorded by this library in the calling thread. */
+const char *lvlip_last_hip_error(void);
+
+/* Diagnostic (bench.py): a plain streaming read of `bytes` (multiple of 16,
+ * 16-B aligned) of device memory, summed into *sink — the achievable HBM read
+ * rate measured beside the checksum kernels.  waves_per_cu 0 = 32. */
+int lvlip_diag_read_probe(const void *src, uint64_t bytes, uint32_t *sink,
+                          int waves_per_cu, void *stream);
+
+#pragma GCC visibility pop
+#ifdef __cplusplus
+}
+#endif
+#endif /* LVLIP_CSUM_H */

@@ -1,0 +1,272 @@
+// csum_ctx.cpp — Group 3 of include/lvlip_csum.h: host-resident batches.
+//
+// level-ip's packets live in malloc'd skb heads (src/skbuff.c:5-20) at offsets
+// 14 (IPv4 header, include/ip.h:47-50) and 34 (TCP/ICMP, include/tcp.h:224-227),
+// i.e. 2 mod 4.  A context owns, per pipeline slot (two slots):
+//   - a pinned host arena the packets are gathered into, each at a 16-B
+//     aligned slot (so the GPU's 16-B chunks never straddle two packets),
+//   - the matching device arena, descriptor and result buffers,
+//   - its own non-blocking stream and a completion event.
+// A batch is cut into arena-sized pieces; piece k is gathered on the CPU while
+// piece k-1's H2D copy, kernel and D2H copy run on the other slot's stream.
+//
+// One context belongs to one thread at a time (no locks on the hot path):
+// the reference calls checksum() from the core, IPC and timer threads
+// (src/main.c:83-89, src/timer.c:74), so each gets its own context.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "lvlip_csum.h"
+
+extern "C" int lvlip_csum_batch_dev_ex(const void*, const lvlip_csum_desc*, uint32_t, uint16_t*,
+                                       void*, const lvlip_launch_cfg*);
+
+namespace {
+
+constexpr size_t kDefaultArena = 64ull << 20;
+constexpr int kSlots = 2;
+
+inline uint64_t align16(uint64_t x) { return (x + 15ull) & ~15ull; }
+
+struct Slot {
+    uint8_t* h_bytes = nullptr;         // pinned
+    lvlip_csum_desc* h_desc = nullptr;  // pinned
+    uint16_t* h_out = nullptr;          // pinned
+    uint8_t* d_bytes = nullptr;
+    lvlip_csum_desc* d_desc = nullptr;
+    uint16_t* d_out = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    // piece bookkeeping
+    uint16_t* user_out = nullptr;  // where results of the in-flight piece go
+    uint32_t count = 0;
+    bool busy = false;
+};
+
+}  // namespace
+
+struct lvlip_csum_ctx {
+    int device = 0;
+    size_t arena = 0;     // bytes per slot
+    uint32_t max_desc = 0;  // descriptors per slot
+    Slot slot[kSlots];
+    char err[256] = "";
+};
+
+namespace {
+
+int fail(lvlip_csum_ctx* c, hipError_t e, const char* what, int code = LVLIP_EHIP) {
+    if (c) snprintf(c->err, sizeof c->err, "%s: %s", what, hipGetErrorString(e));
+    fprintf(stderr, "lvlip_csum: %s: %s\n", what, hipGetErrorString(e));
+    return code;
+}
+
+void free_slot(Slot& s) {
+    if (s.h_bytes) (void)hipHostFree(s.h_bytes);
+    if (s.h_desc) (void)hipHostFree(s.h_desc);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.d_bytes) (void)hipFree(s.d_bytes);
+    if (s.d_desc) (void)hipFree(s.d_desc);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = Slot{};
+}
+
+// Wait for a slot's in-flight piece and hand its results to the caller.
+int drain(lvlip_csum_ctx* c, Slot& s) {
+    if (!s.busy) return LVLIP_OK;
+    hipError_t e = hipEventSynchronize(s.done);
+    s.busy = false;
+    if (e != hipSuccess) return fail(c, e, "hipEventSynchronize");
+    memcpy(s.user_out, s.h_out, (size_t)s.count * sizeof(uint16_t));
+    return LVLIP_OK;
+}
+
+// Copy the gathered piece in `s` to the device, checksum it, copy results back.
+int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uint16_t* user_out) {
+    hipError_t e;
+    if ((e = hipMemcpyAsync(s.d_bytes, s.h_bytes, align16(bytes), hipMemcpyHostToDevice,
+                            s.stream)) != hipSuccess)
+        return fail(c, e, "H2D bytes");
+    if ((e = hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)count * sizeof(lvlip_csum_desc),
+                            hipMemcpyHostToDevice, s.stream)) != hipSuccess)
+        return fail(c, e, "H2D descriptors");
+    lvlip_launch_cfg cfg{};
+    // Gathered pieces are mixed-size skbs by nature; the flat tile sweep keeps
+    // every lane busy on short headers (kernel choice).
+    cfg.kernel = (bytes / count >= 1024) ? LVLIP_KERNEL_WAVE : LVLIP_KERNEL_FLAT;
+    int rc = lvlip_csum_batch_dev_ex(s.d_bytes, s.d_desc, count, s.d_out, s.stream, &cfg);
+    if (rc != LVLIP_OK) return rc;
+    if ((e = hipMemcpyAsync(s.h_out, s.d_out, (size_t)count * sizeof(uint16_t),
+                            hipMemcpyDeviceToHost, s.stream)) != hipSuccess)
+        return fail(c, e, "D2H results");
+    if ((e = hipEventRecord(s.done, s.stream)) != hipSuccess) return fail(c, e, "hipEventRecord");
+    s.user_out = user_out;
+    s.count = count;
+    s.busy = true;
+    return LVLIP_OK;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) {
+    if (!out) return LVLIP_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return LVLIP_ENODEV;
+    if (device < 0 || device >= ndev) return LVLIP_ENODEV;
+    if (arena_bytes == 0) arena_bytes = kDefaultArena;
+    if (arena_bytes < 4096) arena_bytes = 4096;
+    arena_bytes = align16(arena_bytes);
+
+    auto* c = new (std::nothrow) lvlip_csum_ctx();
+    if (!c) return LVLIP_ENOMEM;
+    c->device = device;
+    c->arena = arena_bytes;
+    // worst case one descriptor per 16-B slot (1..16-byte packets)
+    c->max_desc = (uint32_t)(arena_bytes / 16 > LVLIP_MAX_BATCH ? LVLIP_MAX_BATCH : arena_bytes / 16);
+
+    DeviceGuard g(device);
+    for (auto& s : c->slot) {
+        hipError_t e;
+        if ((e = hipHostMalloc((void**)&s.h_bytes, arena_bytes, hipHostMallocDefault)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_desc, (size_t)c->max_desc * sizeof(lvlip_csum_desc),
+                               hipHostMallocDefault)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_out, (size_t)c->max_desc * sizeof(uint16_t),
+                               hipHostMallocDefault)) != hipSuccess ||
+            (e = hipMalloc((void**)&s.d_bytes, arena_bytes)) != hipSuccess ||
+            (e = hipMalloc((void**)&s.d_desc, (size_t)c->max_desc * sizeof(lvlip_csum_desc))) != hipSuccess ||
+            (e = hipMalloc((void**)&s.d_out, (size_t)c->max_desc * sizeof(uint16_t))) != hipSuccess ||
+            (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
+            fail(c, e, "lvlip_csum_ctx_create");
+            for (auto& t : c->slot) free_slot(t);
+            delete c;
+            return LVLIP_ENOMEM;
+        }
+    }
+    *out = c;
+    return LVLIP_OK;
+}
+
+int lvlip_csum_ctx_destroy(lvlip_csum_ctx* c) {
+    if (!c) return LVLIP_EINVAL;
+    DeviceGuard g(c->device);
+    for (auto& s : c->slot) {
+        if (s.busy) (void)hipEventSynchronize(s.done);
+        free_slot(s);
+    }
+    delete c;
+    return LVLIP_OK;
+}
+
+int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_t n,
+                          uint16_t* out) {
+    if (!c || (n && (!pkts || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
+    if (n == 0) return LVLIP_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (pkts[i].len > 0 && (!pkts[i].ptr || align16((uint64_t)pkts[i].len) > c->arena))
+            return LVLIP_ERANGE;  // a single packet larger than the arena
+    DeviceGuard g(c->device);
+
+    int cur = 0;
+    uint32_t i = 0;
+    int rc = LVLIP_OK;
+    while (i < n && rc == LVLIP_OK) {
+        Slot& s = c->slot[cur];
+        if ((rc = drain(c, s)) != LVLIP_OK) break;
+        // gather a piece: packet k at the next 16-B aligned offset
+        uint64_t off = 0;
+        uint32_t k = 0;
+        const uint32_t first = i;
+        while (i < n && k < c->max_desc) {
+            const int32_t len = pkts[i].len;
+            const uint64_t need = len > 0 ? (uint64_t)len : 0;
+            if (off + need > c->arena) break;
+            if (need) memcpy(s.h_bytes + off, pkts[i].ptr, need);
+            s.h_desc[k].offset = off;
+            s.h_desc[k].len = len;
+            s.h_desc[k].start_sum = pkts[i].start_sum;
+            off = align16(off + need);
+            ++k;
+            ++i;
+        }
+        rc = launch_piece(c, s, off ? off : 16, k, out + first);
+        cur ^= 1;
+    }
+    for (auto& s : c->slot) {
+        const int r2 = drain(c, s);
+        if (rc == LVLIP_OK) rc = r2;
+    }
+    return rc;
+}
+
+int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_bytes,
+                               const lvlip_csum_desc* d, uint32_t n, uint16_t* out) {
+    if (!c || (n && (!base || !d || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
+    if (n == 0) return LVLIP_OK;
+    const uint8_t* b = (const uint8_t*)base;
+    DeviceGuard g(c->device);
+
+    int cur = 0;
+    uint32_t i = 0;
+    int rc = LVLIP_OK;
+    while (i < n && rc == LVLIP_OK) {
+        Slot& s = c->slot[cur];
+        if ((rc = drain(c, s)) != LVLIP_OK) break;
+        // A piece is a run of descriptors whose byte span [lo16, hi) fits the
+        // arena.  The span is copied with one memcpy, keeping each packet's
+        // offset mod 16 (so odd/unaligned starts stay exactly as given).
+        const uint32_t first = i;
+        uint64_t lo16 = ~0ull, hi = 0;
+        uint32_t k = 0;
+        while (i < n && k < c->max_desc) {
+            const uint64_t o = d[i].offset;
+            const uint64_t e = o + (d[i].len > 0 ? (uint64_t)d[i].len : 0);
+            if (e > base_bytes) return LVLIP_EINVAL;
+            const uint64_t nlo = (o & ~15ull) < lo16 ? (o & ~15ull) : lo16;
+            const uint64_t nhi = e > hi ? e : hi;
+            if (align16(nhi) - nlo > c->arena) {
+                if (k == 0) return LVLIP_ERANGE;
+                break;
+            }
+            lo16 = nlo;
+            hi = nhi;
+            ++k;
+            ++i;
+        }
+        const uint64_t span = hi > lo16 ? hi - lo16 : 0;
+        if (span) memcpy(s.h_bytes, b + lo16, span);
+        for (uint32_t q = 0; q < k; ++q) {
+            s.h_desc[q] = d[first + q];
+            s.h_desc[q].offset = d[first + q].offset - lo16;
+        }
+        rc = launch_piece(c, s, span ? span : 16, k, out + first);
+        cur ^= 1;
+    }
+    for (auto& s : c->slot) {
+        const int r2 = drain(c, s);
+        if (rc == LVLIP_OK) rc = r2;
+    }
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,276 @@
+"""lvlip — ctypes binding of liblvlip_csum.so (include/lvlip_csum.h).
+
+Host-side mirror of level-ip's checksum interface for tests/ and bench.py.
+The names follow the reference:
+
+  checksum(buf, count, start_sum)      src/utils.c:40-55  (include/utils.h:14)
+  sum_every_16bits(buf, count)         src/utils.c:22-38  (include/utils.h:13)
+  tcp_udp_checksum(saddr, daddr, proto, data, len)   src/tcp.c:87-98
+  ip_send_check(iphdr_bytearray)       src/ip_output.c:8-12
+
+plus the batched GPU entry points (batch_dev, Context.batch_host[_flat]).
+
+The library is loaded eagerly and a missing or broken build raises
+LvlipUnavailable: there is no Python or CPU fallback for the batched path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblvlip_csum.so")
+TESTKIT_PATH = os.path.join(HERE, "liblvlip_testkit.so")
+
+# error codes (include/lvlip_csum.h)
+OK, EINVAL, ENODEV, EHIP, ENOMEM, ERANGE = 0, -1, -2, -3, -4, -5
+KERNEL_AUTO, KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_FLAT = 0, 1, 2, 3
+KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "wave_lds": KERNEL_WAVE_LDS,
+                "flat": KERNEL_FLAT}
+
+# struct lvlip_csum_desc {u64 offset; i32 len; u32 start_sum;}  (16 B)
+DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<i4"), ("start_sum", "<u4")])
+assert DESC_DTYPE.itemsize == 16
+
+
+class LvlipUnavailable(RuntimeError):
+    """liblvlip_csum.so is missing or cannot be loaded."""
+
+
+class LvlipError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        self.rc = rc
+        detail = ""
+        try:
+            detail = _lib.lvlip_last_hip_error().decode()
+        except Exception:  # pragma: no cover
+            pass
+        msg = f"{what}: {_lib.lvlip_strerror(rc).decode()} ({rc})"
+        if detail:
+            msg += f" [{detail}]"
+        super().__init__(msg)
+
+
+class LaunchCfg(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_int32), ("unroll", ctypes.c_int32),
+                ("waves_per_cu", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class Iov(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("len", ctypes.c_int32), ("start_sum", ctypes.c_uint32)]
+
+
+def _load(path: str) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise LvlipUnavailable(
+            f"{path} not built: run `make -C level-ip_amd` (or __graft_entry__.build())")
+    try:
+        return ctypes.CDLL(path)
+    except OSError as e:  # pragma: no cover
+        raise LvlipUnavailable(f"cannot load {path}: {e}") from e
+
+
+_lib = _load(LIB_PATH)
+
+# every entry point declared in include/lvlip_csum.h, with its ctypes signature
+SIGNATURES = {
+    "sum_every_16bits": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_int]),
+    "checksum": (ctypes.c_uint16, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "lvlip_pseudo_sum": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8,
+                                            ctypes.c_uint16]),
+    "lvlip_csum_batch_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                            ctypes.c_void_p, ctypes.c_void_p]),
+    "lvlip_csum_batch_dev_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                               ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.POINTER(LaunchCfg)]),
+    "lvlip_csum_ctx_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                             ctypes.c_size_t]),
+    "lvlip_csum_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "lvlip_csum_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Iov), ctypes.c_uint32,
+                                             ctypes.c_void_p]),
+    "lvlip_csum_batch_host_flat": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                  ctypes.c_void_p, ctypes.c_uint32,
+                                                  ctypes.c_void_p]),
+    "lvlip_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "lvlip_abi_version": (ctypes.c_int, []),
+    "lvlip_device_count": (ctypes.c_int, []),
+    "lvlip_last_hip_error": (ctypes.c_char_p, []),
+    "lvlip_diag_read_probe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                             ctypes.c_int, ctypes.c_void_p]),
+}
+for _name, (_res, _args) in SIGNATURES.items():
+    _fn = getattr(_lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+def lib() -> ctypes.CDLL:
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != OK:
+        raise LvlipError(rc, what)
+
+
+def _as_u8(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+    return np.frombuffer(bytes(buf), dtype=np.uint8)
+
+
+# --------------------------------------------------------------- per call --
+
+def sum_every_16bits(buf, count: Optional[int] = None) -> int:
+    a = _as_u8(buf)
+    if count is None:
+        count = a.size
+    if count > a.size:
+        raise ValueError("count exceeds buffer")
+    return int(_lib.sum_every_16bits(a.ctypes.data if a.size else None, int(count)))
+
+
+def checksum(buf, count: Optional[int] = None, start_sum: int = 0) -> int:
+    """src/utils.c:40-55; start_sum is the reference's `int` (any u32 bit pattern)."""
+    a = _as_u8(buf)
+    if count is None:
+        count = a.size
+    if count > a.size:
+        raise ValueError("count exceeds buffer")
+    s = ctypes.c_int(ctypes.c_uint32(start_sum & 0xFFFFFFFF).value).value
+    return int(_lib.checksum(a.ctypes.data if a.size else None, int(count), s))
+
+
+def pseudo_sum(saddr: int, daddr: int, proto: int, length: int) -> int:
+    """Seed of tcp_udp_checksum (src/tcp.c:87-96), u32 wrap-around."""
+    return int(_lib.lvlip_pseudo_sum(saddr & 0xFFFFFFFF, daddr & 0xFFFFFFFF, proto & 0xFF,
+                                     length & 0xFFFF))
+
+
+def tcp_udp_checksum(saddr: int, daddr: int, proto: int, data, length: int) -> int:
+    """src/tcp.c:87-98 (len is a uint16_t there, so it is truncated the same way)."""
+    length &= 0xFFFF
+    return checksum(data, length, pseudo_sum(saddr, daddr, proto, length))
+
+
+def ip_send_check(hdr: bytearray) -> None:
+    """src/ip_output.c:8-12: checksum over ihl*4 bytes, stored raw at offset 10."""
+    ihl = hdr[0] & 0x0F
+    c = checksum(bytes(hdr[: ihl * 4]), ihl * 4, 0)
+    hdr[10:12] = int(c).to_bytes(2, "little")
+
+
+# ---------------------------------------------------------- device batches --
+
+def batch_dev(base_ptr: int, desc_ptr: int, n: int, out_ptr: int, stream: int = 0,
+              kernel: int = KERNEL_AUTO, unroll: int = 0, waves_per_cu: int = 0) -> None:
+    """lvlip_csum_batch_dev_ex on raw device pointers (async on `stream`)."""
+    cfg = LaunchCfg(kernel, unroll, waves_per_cu, 0)
+    _check(_lib.lvlip_csum_batch_dev_ex(base_ptr, desc_ptr, n, out_ptr, stream or None,
+                                        ctypes.byref(cfg)), "lvlip_csum_batch_dev_ex")
+
+
+def batch_torch(base, descs, out=None, kernel: int = KERNEL_AUTO, unroll: int = 0,
+                waves_per_cu: int = 0, stream=None):
+    """Checksums a device batch held in torch tensors on the current stream.
+
+    base:  uint8 CUDA tensor (16-B aligned, padded to a 16-B multiple past the last packet)
+    descs: CUDA tensor of n*16 bytes (uint8 or int64 view of lvlip_csum_desc[n])
+    out:   int16/uint16 CUDA tensor of n elements (allocated when None)
+    """
+    import torch
+
+    if not (base.is_cuda and descs.is_cuda):
+        raise ValueError("batch_torch needs CUDA tensors")
+    n = descs.numel() * descs.element_size() // 16
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=base.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(base.device)
+    batch_dev(base.data_ptr(), descs.data_ptr(), n, out.data_ptr(), stream.cuda_stream,
+              kernel, unroll, waves_per_cu)
+    return out
+
+
+def read_probe(src_ptr: int, nbytes: int, sink_ptr: int, waves_per_cu: int = 0,
+               stream: int = 0) -> None:
+    _check(_lib.lvlip_diag_read_probe(src_ptr, nbytes, sink_ptr, waves_per_cu, stream or None),
+           "lvlip_diag_read_probe")
+
+
+def device_count() -> int:
+    return int(_lib.lvlip_device_count())
+
+
+# ------------------------------------------------------------ host batches --
+
+class Context:
+    """lvlip_csum_ctx: pinned arena + device arena + streams, one thread at a time."""
+
+    def __init__(self, device: int = 0, arena_bytes: int = 0):
+        self._h = ctypes.c_void_p()
+        _check(_lib.lvlip_csum_ctx_create(ctypes.byref(self._h), device, arena_bytes),
+               "lvlip_csum_ctx_create")
+
+    def close(self) -> None:
+        if self._h:
+            _lib.lvlip_csum_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def batch_host(self, packets: Sequence, start_sums: Sequence[int]) -> np.ndarray:
+        """packets: sequence of bytes-like / uint8 arrays (the skb payloads)."""
+        n = len(packets)
+        keep = [_as_u8(p) for p in packets]
+        iov = (Iov * n)()
+        for i, (a, s) in enumerate(zip(keep, start_sums)):
+            iov[i].ptr = a.ctypes.data if a.size else None
+            iov[i].len = a.size
+            iov[i].start_sum = s & 0xFFFFFFFF
+        out = np.empty(n, dtype=np.uint16)
+        _check(_lib.lvlip_csum_batch_host(self._h, iov, n, out.ctypes.data),
+               "lvlip_csum_batch_host")
+        return out
+
+    def batch_host_flat(self, base: np.ndarray, descs: np.ndarray) -> np.ndarray:
+        base = _as_u8(base)
+        descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+        n = descs.size
+        out = np.empty(n, dtype=np.uint16)
+        _check(_lib.lvlip_csum_batch_host_flat(self._h, base.ctypes.data, base.size,
+                                               descs.ctypes.data, n, out.ctypes.data),
+               "lvlip_csum_batch_host_flat")
+        return out
+
+
+# ------------------------------------------------------------------ testkit --
+
+_testkit = None
+
+
+def testkit() -> ctypes.CDLL:
+    global _testkit
+    if _testkit is None:
+        tk = _load(TESTKIT_PATH)
+        tk.lvlip_testkit_fill.restype = ctypes.c_int
+        tk.lvlip_testkit_fill.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                          ctypes.c_uint64, ctypes.c_void_p]
+        tk.lvlip_testkit_paint.restype = ctypes.c_int
+        tk.lvlip_testkit_paint.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.c_void_p]
+        _testkit = tk
+    return _testkit

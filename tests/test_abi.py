@@ -1,0 +1,91 @@
+"""The C-ABI boundary: the library loads, exports exactly what include/*.h
+declares, and rejects bad arguments without touching a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import lvlip
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "lvlip_csum.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\(", src, flags=re.M)
+    return sorted(set(n for n in names if n not in ("defined",)))
+
+
+def test_header_declares_the_reference_names():
+    names = declared_functions()
+    # include/utils.h:13-14 drop-ins
+    assert "checksum" in names and "sum_every_16bits" in names
+    for n in ("lvlip_csum_batch_dev", "lvlip_csum_batch_dev_ex", "lvlip_csum_batch_host",
+              "lvlip_csum_batch_host_flat", "lvlip_csum_ctx_create", "lvlip_csum_ctx_destroy",
+              "lvlip_pseudo_sum"):
+        assert n in names
+
+
+def test_every_declared_symbol_is_exported():
+    names = declared_functions()
+    exported = subprocess.run(["nm", "-D", "--defined-only", lvlip.LIB_PATH], check=True,
+                              capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in exported.splitlines() if " T " in l}
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    # and nothing else leaks (kernel stubs, C++ helpers)
+    extra = sorted(exported - set(names))
+    assert not extra, extra
+    for n in names:
+        assert hasattr(lvlip.lib(), n)
+
+
+def test_header_is_plain_c():
+    # compiles as C99 with no HIP/torch headers on the include path
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c", "-"],
+                       input=f'#include "{HEADER}"\nint main(void){{return 0;}}\n', text=True,
+                       capture_output=True)
+    assert r.returncode == 0, r.stderr
+    body = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    assert not re.search(r"\bhip\w*_t\b|#include\s*<hip", body)
+    assert "torch" not in body.lower()
+
+
+def test_desc_layout():
+    assert lvlip.DESC_DTYPE.itemsize == 16
+    assert ctypes.sizeof(lvlip.LaunchCfg) == 16
+    assert lvlip.lib().lvlip_abi_version() == 1
+
+
+def test_error_paths_without_gpu():
+    L = lvlip.lib()
+    out = np.zeros(4, dtype=np.uint16)
+    # NULL pointers / misaligned base -> EINVAL before any HIP call
+    assert L.lvlip_csum_batch_dev(None, None, 4, out.ctypes.data, None) == lvlip.EINVAL
+    assert L.lvlip_csum_batch_dev(1, 16, 4, out.ctypes.data, None) == lvlip.EINVAL
+    # n == 0 is a no-op success
+    assert L.lvlip_csum_batch_dev(None, None, 0, None, None) == lvlip.OK
+    assert L.lvlip_csum_ctx_destroy(None) == lvlip.EINVAL
+    assert L.lvlip_strerror(lvlip.ERANGE) == b"batch exceeds context arena"
+    cfg = lvlip.LaunchCfg(99, 0, 0, 0)
+    assert L.lvlip_csum_batch_dev_ex(16 * 1024, 16, 1, 16, None, ctypes.byref(cfg)) == lvlip.EINVAL
+
+
+def test_no_device_context_fails_loudly():
+    if lvlip.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(lvlip.LvlipError) as e:
+        lvlip.Context(0)
+    assert "no HIP device" in str(e.value)
+
+
+def test_gfx950_code_object_present():
+    # the kernels are cross-compiled for gfx950 only (no other offload targets)
+    blob = open(lvlip.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx\w+)", blob))
+    assert targets == {b"gfx950"}, targets

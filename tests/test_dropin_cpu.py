@@ -1,0 +1,86 @@
+"""Group 1 of include/lvlip_csum.h — the per-call drop-in for src/utils.c:22-55 —
+against the reference's outputs, plus BASELINE config #1 (ICMPv4 echo through
+the reference stack with a fake TAP, CPU only)."""
+import numpy as np
+
+import golden_io
+import lvlip
+
+
+def test_kats():
+    cases, tcp = golden_io.kats()
+    for name, data, count, start, expected in cases:
+        assert lvlip.checksum(data if data else b"\0", count, start) == expected, name
+    for t in tcp:
+        got = lvlip.tcp_udp_checksum(t["saddr"], t["daddr"], t["proto"],
+                                     bytes.fromhex(t["data_hex"]), t["len"])
+        assert got == t["expected"], t["name"]
+
+
+def test_vectors():
+    v = golden_io.vectors()
+    blob = v["blob"]
+    for off, ln, st, exp in zip(v["offset"], v["len"], v["start_sum"], v["expected"]):
+        off, ln = int(off), int(ln)
+        got = lvlip.checksum(blob[off:], ln, int(st))
+        assert got == int(exp), (off, ln, int(st))
+
+
+def test_sum_every_16bits_matches_definition():
+    rng = np.random.default_rng(3)
+    for ln in list(range(0, 40)) + [255, 256, 257, 4095, 65535, 262145, 1 << 20]:
+        a = rng.integers(0, 256, max(ln, 1), dtype=np.uint8)
+        words = a[: ln & ~1].view("<u2").astype(np.uint64).sum()
+        if ln & 1:
+            words += int(a[ln - 1])
+        assert lvlip.sum_every_16bits(a, ln) == int(words) & 0xFFFFFFFF
+    # a sum that overflows u32 (the reference wraps silently)
+    big = np.full(70000 * 2 * 32, 0xFF, dtype=np.uint8)
+    n = big.size
+    assert lvlip.sum_every_16bits(big, n) == (0xFFFF * (n // 2)) & 0xFFFFFFFF
+
+
+def test_tcp_vectors():
+    t = golden_io.tcp()
+    for i in range(t["len"].size):
+        off, ln = int(t["offset"][i]), int(t["len"][i])
+        got = lvlip.tcp_udp_checksum(int(t["saddr"][i]), int(t["daddr"][i]), int(t["proto"][i]),
+                                     t["blob"][off:off + max(ln, 1)], ln)
+        assert got == int(t["expected"][i]), i
+
+
+def test_ip_send_check():
+    h = golden_io.iphdr()
+    for hdr, after in zip(h["hdr"], h["after"]):
+        b = bytearray(hdr.tobytes())
+        lvlip.ip_send_check(b)
+        assert bytes(b) == after.tobytes()
+
+
+def test_echo_config1_cpu():
+    """Config #1: the reference stack's replies re-derived with the drop-in.
+
+    For each request frame: the IPv4 header verifies to 0 (src/ip_input.c:38);
+    the reply's ICMP checksum equals checksum(icmp with csum=0)
+    (src/icmpv4.c:46-47) and its IPv4 header checksum equals ip_send_check's
+    (src/ip_output.c:42,53) — both compared with the bytes the reference wrote."""
+    e = golden_io.echo()
+    assert len(e["echo"]) >= 2
+    for case in e["echo"]:
+        req = bytes.fromhex(case["request_hex"])
+        rep = bytearray(bytes.fromhex(case["reply_hex"]))
+        assert lvlip.checksum(req[14:34], 20, 0) == 0
+        iplen = int.from_bytes(rep[16:18], "big")
+        icmp = bytearray(rep[34:14 + iplen])
+        want_icmp = int.from_bytes(icmp[2:4], "little")
+        icmp[2:4] = b"\0\0"
+        assert icmp[0] == 0  # echo reply
+        assert lvlip.checksum(bytes(icmp), len(icmp), 0) == want_icmp
+        hdr = bytearray(rep[14:34])
+        want_ip = bytes(hdr[10:12])
+        hdr[10:12] = b"\0\0"
+        lvlip.ip_send_check(hdr)
+        assert bytes(hdr[10:12]) == want_ip
+        # and the full reply verifies
+        assert lvlip.checksum(bytes(rep[14:34]), 20, 0) == 0
+        assert lvlip.checksum(bytes(rep[34:14 + iplen]), iplen - 20, 0) == 0

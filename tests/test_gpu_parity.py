@@ -1,0 +1,266 @@
+"""GPU parity: every kernel of liblvlip_csum.so against the reference's outputs
+(tests/golden) and the oracle, bit for bit, through the C-ABI.
+
+Sizes: the golden fixtures, small seeded batches of each BASELINE config, and
+the full 1 M x 1500 B / 1 M x 9000 B / 2 M-frame mixed batches, where every one
+of the N outputs is compared with the oracle run over the same bytes copied back
+from HBM.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import golden_io
+import lvlip
+import pyoracle
+import workloads
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+THREADS = min(16, os.cpu_count() or 1)
+# (kernel, unroll, waves_per_cu)
+VARIANTS = [
+    (lvlip.KERNEL_AUTO, 0, 0),
+    (lvlip.KERNEL_WAVE, 1, 0),
+    (lvlip.KERNEL_WAVE, 2, 0),
+    (lvlip.KERNEL_WAVE, 4, 0),
+    (lvlip.KERNEL_WAVE, 8, 0),
+    (lvlip.KERNEL_WAVE, 2, 16),   # persistent grid-stride form
+    (lvlip.KERNEL_WAVE_LDS, 1, 0),
+    (lvlip.KERNEL_WAVE_LDS, 2, 0),
+    (lvlip.KERNEL_WAVE_LDS, 4, 8),
+    (lvlip.KERNEL_FLAT, 0, 0),
+]
+VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available() or lvlip.device_count() == 0:
+        pytest.fail("GPU tests need a HIP device (run them on the MI355X box)")
+
+
+def dev_blob(a: np.ndarray, pad: int = 64):
+    n = (a.size + pad + 15) & ~15
+    t = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    t[: a.size] = torch.from_numpy(np.ascontiguousarray(a))
+    return t
+
+
+def dev_descs(d: np.ndarray):
+    d = np.ascontiguousarray(d, dtype=lvlip.DESC_DTYPE)
+    return torch.from_numpy(d.view(np.uint8).copy()).to("cuda")
+
+
+def run(base, descs, variant, out=None):
+    k, u, w = variant
+    out = lvlip.batch_torch(base, descs, out, kernel=k, unroll=u, waves_per_cu=w)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint16)
+
+
+def mk_descs(off, ln, st):
+    d = np.zeros(len(off), dtype=lvlip.DESC_DTYPE)
+    d["offset"], d["len"], d["start_sum"] = off, ln, st
+    return d
+
+
+@pytest.mark.parametrize("variant", VARIANTS, ids=VID)
+def test_golden_vectors(variant):
+    v = golden_io.vectors()
+    base = dev_blob(v["blob"])
+    d = mk_descs(v["offset"], v["len"], v["start_sum"])
+    got = run(base, dev_descs(d), variant)
+    bad = np.nonzero(got != v["expected"])[0]
+    assert bad.size == 0, [(int(v["offset"][i]), int(v["len"][i]), hex(got[i]),
+                            hex(v["expected"][i])) for i in bad[:8]]
+
+
+@pytest.mark.parametrize("variant", VARIANTS, ids=VID)
+def test_kats_every_alignment(variant):
+    cases, tcp = golden_io.kats()
+    blob, off, ln, st, exp = bytearray(), [], [], [], []
+    for name, data, count, start, expected in cases:
+        for mis in (0, 1, 2, 3, 7, 14, 15):
+            while len(blob) % 16 != mis:
+                blob.append(0xA5)
+            off.append(len(blob))
+            blob += data
+            ln.append(count)
+            st.append(start)
+            exp.append(expected)
+    for t in tcp:
+        off.append(len(blob))
+        blob += bytes.fromhex(t["data_hex"])
+        ln.append(t["len"])
+        st.append(lvlip.pseudo_sum(t["saddr"], t["daddr"], t["proto"], t["len"]))
+        exp.append(t["expected"])
+    got = run(dev_blob(np.frombuffer(bytes(blob), dtype=np.uint8)),
+              dev_descs(mk_descs(off, ln, st)), variant)
+    assert list(got) == exp
+
+
+def test_tcp_golden():
+    t = golden_io.tcp()
+    ln = t["len"].astype(np.int32)
+    st = np.array([lvlip.pseudo_sum(int(a), int(b), int(p), int(l))
+                   for a, b, p, l in zip(t["saddr"], t["daddr"], t["proto"], t["len"])],
+                  dtype=np.uint32)
+    d = mk_descs(t["offset"], ln, st)
+    base, descs = dev_blob(t["blob"]), dev_descs(d)
+    for variant in VARIANTS:
+        got = run(base, descs, variant)
+        assert np.array_equal(got, t["expected"]), variant
+
+
+def test_ip_headers_golden():
+    h = golden_io.iphdr()
+    hdr = h["hdr"].copy()
+    n = hdr.shape[0]
+    blob = np.zeros((n, 64), dtype=np.uint8)
+    blob[:, 2:62] = hdr  # 2 mod 4, like skb->head + 14
+    ihl = (hdr[:, 0] & 0xF).astype(np.int32)
+    d = mk_descs(np.arange(n) * 64 + 2, ihl * 4, np.zeros(n, dtype=np.uint32))
+    for variant in VARIANTS:
+        got = run(dev_blob(blob.reshape(-1)), dev_descs(d), variant)
+        want = h["after"][:, 10].astype(np.uint16) | (h["after"][:, 11].astype(np.uint16) << 8)
+        assert np.array_equal(got, want), variant
+
+
+def test_echo_config1_on_gpu():
+    """Config #1's three checksums (IPv4 RX verify, ICMP reply, IPv4 TX) as one
+    device batch over the reference's frames; compared with its reply bytes."""
+    e = golden_io.echo()
+    blob, off, ln, exp = bytearray(), [], [], []
+    for case in e["echo"]:
+        req = bytes.fromhex(case["request_hex"])
+        rep = bytearray(bytes.fromhex(case["reply_hex"]))
+        iplen = int.from_bytes(rep[16:18], "big")
+        want_icmp = int.from_bytes(rep[36:38], "little")
+        want_ip = int.from_bytes(rep[24:26], "little")
+        rep[36:38] = b"\0\0"
+        rep[24:26] = b"\0\0"
+        base_req = len(blob)
+        blob += req
+        base_rep = len(blob)
+        blob += rep
+        while len(blob) % 16:
+            blob.append(0)
+        off += [base_req + 14, base_rep + 34, base_rep + 14]
+        ln += [20, iplen - 20, 20]
+        exp += [0, want_icmp, want_ip]
+    got = run(dev_blob(np.frombuffer(bytes(blob), dtype=np.uint8)),
+              dev_descs(mk_descs(off, ln, [0] * len(off))), (lvlip.KERNEL_AUTO, 0, 0))
+    assert list(got) == exp
+
+
+def test_alignment_length_sweep():
+    rng = np.random.default_rng(11)
+    blob = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    off, ln = np.meshgrid(np.arange(0, 48), np.arange(0, 300))
+    off = (off.reshape(-1) + 1000).astype(np.uint64)
+    ln = ln.reshape(-1).astype(np.int32)
+    st = rng.integers(0, 2**32, off.size, dtype=np.uint64).astype(np.uint32)
+    d = mk_descs(off, ln, st)
+    want = pyoracle.batch(blob, d)
+    base, descs = dev_blob(blob), dev_descs(d)
+    for variant in VARIANTS:
+        assert np.array_equal(run(base, descs, variant), want), variant
+
+
+@pytest.mark.parametrize("name,n", [("tcp1500", 20000), ("tcp9000", 3000), ("mixed", 20000)])
+def test_configs_small_all_kernels(name, n):
+    b = workloads.make(name, n=n)
+    base, descs, out = workloads.to_device(b)
+    host = base.cpu().numpy()
+    assert np.array_equal(host[: b.nbytes], b.host_bytes()), "device fill != host fill"
+    want = pyoracle.batch(host, b.descs, threads=THREADS)
+    for variant in VARIANTS:
+        got = run(base, descs, variant, out)
+        assert np.array_equal(got, want), variant
+
+
+@pytest.mark.parametrize("name", ["tcp1500", "tcp9000", "mixed"])
+def test_full_size_bit_exact(name):
+    """BASELINE configs #2-#4 at full size: all N outputs vs the oracle on the same bytes."""
+    b = workloads.make(name)
+    base, descs, out = workloads.to_device(b)
+    got_auto = run(base, descs, (lvlip.KERNEL_AUTO, 0, 0), out)
+    host = base.cpu().numpy()
+    want = pyoracle.batch(host, b.descs, threads=THREADS)
+    bad = np.nonzero(got_auto != want)[0]
+    assert bad.size == 0, f"{bad.size} of {b.n} differ; first {bad[:5]}"
+    # size-independent property: every kernel variant agrees, and reruns are identical
+    for variant in [(lvlip.KERNEL_WAVE, 4, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
+                    (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_AUTO, 0, 0)]:
+        assert np.array_equal(run(base, descs, variant, out), want), variant
+    # adversarial packets really are there and fold as the reference does
+    ones = b.paint == 2
+    zeros = b.paint == 1
+    assert ones.any() and zeros.any()
+    del base, descs, out
+    torch.cuda.empty_cache()
+
+
+def test_empty_and_tiny_batches():
+    base = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    descs = dev_descs(mk_descs([0], [0], [0]))
+    for variant in VARIANTS:
+        assert list(run(base, descs, variant)) == [0xFFFF]
+    out = torch.empty(0, dtype=torch.int16, device="cuda")
+    lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), 0, out.data_ptr())
+
+
+def test_misaligned_base_rejected():
+    base = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    descs = dev_descs(mk_descs([0], [4], [0]))
+    out = torch.empty(1, dtype=torch.int16, device="cuda")
+    with pytest.raises(lvlip.LvlipError):
+        lvlip.batch_dev(base.data_ptr() + 2, descs.data_ptr(), 1, out.data_ptr())
+
+
+# ----------------------------------------------------------- host batches --
+
+def test_host_iov_ragged_unaligned():
+    rng = np.random.default_rng(5)
+    pool = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    pkts, starts, want = [], [], []
+    for i in range(4000):
+        ln = int(rng.integers(0, 1600)) if i % 7 else int(rng.integers(0, 9100))
+        off = int(rng.integers(0, pool.size - ln))  # any address, odd ones included
+        pkts.append(pool[off:off + ln])
+        st = int(rng.integers(0, 2**32))
+        starts.append(st)
+        want.append(pyoracle.checksum(pool[off:off + max(ln, 1)], ln, st))
+    # a small arena forces many double-buffered pieces
+    with lvlip.Context(0, arena_bytes=256 << 10) as ctx:
+        got = ctx.batch_host(pkts, starts)
+    assert list(got) == want
+    with lvlip.Context(0) as ctx:
+        assert list(ctx.batch_host(pkts, starts)) == want
+
+
+def test_host_flat_config_slices():
+    b = workloads.make("mixed", n=30000)
+    host = b.host_bytes()
+    want = pyoracle.batch(host, b.descs, threads=THREADS)
+    with lvlip.Context(0, arena_bytes=1 << 20) as ctx:
+        assert np.array_equal(ctx.batch_host_flat(host, b.descs), want)
+    b = workloads.make("tcp1500", n=50000)
+    host = b.host_bytes()
+    want = pyoracle.batch(host, b.descs, threads=THREADS)
+    with lvlip.Context(0) as ctx:
+        assert np.array_equal(ctx.batch_host_flat(host, b.descs), want)
+
+
+def test_read_probe_sums():
+    a = torch.arange(0, 1 << 20, dtype=torch.int32, device="cuda")
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    lvlip.read_probe(a.data_ptr(), a.numel() * 4, sink.data_ptr(), 8,
+                     torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    h = a.cpu().numpy().view(np.uint16).astype(np.uint64).sum() & 0xFFFFFFFF
+    assert int(sink.item()) & 0xFFFFFFFF == int(h)
