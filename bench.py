@@ -27,6 +27,7 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "level-ip_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))  # cpu_baseline leg only (pyoracle)
 
 import numpy as np  # noqa: E402
 
@@ -49,7 +50,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--workload", default="tcp1500", choices=sorted(WORKLOAD_TEXT))
     p.add_argument("--n", type=int, default=None, help="packets (frames for mixed) per rank")
-    p.add_argument("--kernel", default="auto", choices=["auto", "wave", "wave_lds", "flat"])
+    p.add_argument("--kernel", default="auto",
+                   choices=["auto", "wave", "wave_lds", "flat", "wave_simple"])
     p.add_argument("--unroll", type=int, default=0)
     p.add_argument("--waves-per-cu", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -257,9 +259,8 @@ def timed(torch, fn, stream, reps=20, warm=3):
 
 def sweep(lvlip, torch, base, descs, out, b, stream):
     res = {}
-    variants = [("wave", 1, 0), ("wave", 2, 0), ("wave", 4, 0), ("wave", 8, 0), ("wave", 2, 8),
-                ("wave", 2, 16), ("wave", 4, 16), ("wave", 4, 32), ("wave_lds", 1, 0),
-                ("wave_lds", 2, 0), ("wave_lds", 4, 0), ("wave_lds", 2, 16), ("flat", 0, 0)]
+    variants = [("wave", 2, 8), ("wave", 4, 4), ("wave", 4, 8), ("wave", 4, 16), ("wave", 8, 4),
+                ("wave", 8, 8), ("wave_simple", 2, 0), ("wave_lds", 2, 0), ("flat", 0, 0)]
     for rnd in range(2):  # interleaved rounds in one process
         for k, u, w in variants:
             def f():
@@ -274,15 +275,21 @@ def sweep(lvlip, torch, base, descs, out, b, stream):
 
 
 def read_probe(lvlip, torch, base, stream):
-    """Achievable streaming-read rate over the same buffer (diagnostic)."""
+    """Achievable streaming-read rate over the same buffer (lab probe; diagnostic)."""
+    try:
+        lab = lvlip.lab()
+    except lvlip.LvlipUnavailable:
+        return None
     sink = torch.zeros(1, dtype=torch.int32, device=base.device)
-    nb = base.numel() & ~15
+    nb = base.numel() & ~1023
+    cus = torch.cuda.get_device_properties(base.device).multi_processor_count
     best = {}
-    for w in (8, 16, 32):
-        ms = timed(torch, lambda: lvlip.read_probe(base.data_ptr(), nb, sink.data_ptr(), w,
-                                                   stream.cuda_stream), stream, reps=10)
-        best[w] = round(nb / ms / 1e6, 1)
-    log("read_probe GB/s by waves/CU", best)
+    for mode, u, nt, bpc in ((1, 4, 1, 4), (1, 8, 1, 2), (3, 4, 0, 4)):
+        ms = timed(torch, lambda: lab.lvlip_lab_probe(base.data_ptr(), nb, sink.data_ptr(), mode, u,
+                                                      nt, cus * bpc, stream.cuda_stream),
+                   stream, reps=10)
+        best[f"m{mode}u{u}nt{nt}b{bpc}"] = round(nb / ms / 1e6, 1)
+    log("read_probe GB/s", best)
     return best
 
 

@@ -100,15 +100,17 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
                          uint32_t n, uint16_t *out, void *stream);
 
 /* Kernel selection for lvlip_csum_batch_dev_ex (benchmarks, A/B tests). */
-#define LVLIP_KERNEL_AUTO      0  /* the default (kernel choice)   */
-#define LVLIP_KERNEL_WAVE      1  /* one wavefront per packet, VGPR staging       */
-#define LVLIP_KERNEL_WAVE_LDS  2  /* one wavefront per packet, LDS-DMA staging    */
-#define LVLIP_KERNEL_FLAT      3  /* chunk-balanced tile sweep (ragged batches)   */
+#define LVLIP_KERNEL_AUTO        0  /* the default (kernel choice)  */
+#define LVLIP_KERNEL_WAVE        1  /* one wavefront per packet, persistent stream */
+#define LVLIP_KERNEL_WAVE_LDS    2  /* one wave per packet, LDS-DMA staging (A/B)  */
+#define LVLIP_KERNEL_FLAT        3  /* chunk-balanced tile sweep (ragged batches)  */
+#define LVLIP_KERNEL_WAVE_SIMPLE 4  /* one wave per packet, one launch wave each   */
 
 typedef struct lvlip_launch_cfg {
     int32_t  kernel;        /* LVLIP_KERNEL_*                               */
     int32_t  unroll;        /* 16-B loads in flight per lane (0 = default)  */
-    int32_t  waves_per_cu;  /* grid size knob, 0 = one wave per packet      */
+    int32_t  waves_per_cu;  /* WAVE: resident waves per CU (0 = 8); others:
+                               grid cap (0 = one wave per packet)           */
     int32_t  reserved;      /* must be 0                                    */
 } lvlip_launch_cfg;
 
@@ -162,12 +164,6 @@ int lvlip_abi_version(void);
 int lvlip_device_count(void);
 /* Last HIP error string recorded by this library in the calling thread. */
 const char *lvlip_last_hip_error(void);
-
-/* Diagnostic (bench.py): a plain streaming read of `bytes` (multiple of 16,
- * 16-B aligned) of device memory, summed into *sink — the achievable HBM read
- * rate measured beside the checksum kernels.  waves_per_cu 0 = 32. */
-int lvlip_diag_read_probe(const void *src, uint64_t bytes, uint32_t *sink,
-                          int waves_per_cu, void *stream);
 
 #pragma GCC visibility pop
 #ifdef __cplusplus

@@ -84,6 +84,42 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
+// 64-lane u32 sum with DPP (no LDS traffic); the total is returned uniform
+// (SGPR) from lane 63.  quad_perm(1,0,3,2), quad_perm(2,3,0,1), row_ror:4,
+// row_ror:8 leave every lane holding its 16-lane row sum; row_bcast:15 (rows 1,3)
+// and row_bcast:31 (rows 2,3) accumulate the four rows into lane 63.  Lanes of
+// rows a row_mask leaves out keep `old` = 0, so the adds there are no-ops.
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Streaming (read-once) 16-B load: `global_load_dwordx4 ... nt`.  The batch is
+// read exactly once, so keeping it out of the caches' retained set is worth
+// ~+8 % read bandwidth on MI355X (scripts/lab_read.py).
+__device__ __forceinline__ uint4 load_nt(const uint8_t* p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Wait until at most N vector-memory operations are outstanding.  The slot's
+// register is an in/out operand, so no instruction that reads it can be
+// scheduled above the wait (a plain asm barrier does not order register-only
+// instructions, cdna_hip_programming.md §5.4 rule 18).
+template <int N>
+__device__ __forceinline__ void ring_wait(u32x4& r) {
+    // "memory": LDS reads of descriptor windows (retired by these same waits)
+    // must not move above it either.
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r) : "n"(N) : "memory");
+}
+
 // utils.c:46-54.  Two unconditional folds equal the reference's while loop:
 // after the first T <= 0x1fffe, after the second T <= 0xffff, and a fold of a
 // value <= 0xffff is the identity.
@@ -128,7 +164,7 @@ __device__ __forceinline__ uint32_t wave_packet_sum(const uint4* __restrict__ sr
 }
 
 template <int U>
-__global__ __launch_bounds__(256) void k_wave(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(256) void k_wave_simple(const uint8_t* __restrict__ base,
                                               const lvlip_csum_desc* __restrict__ descs,
                                               uint32_t n, uint16_t* __restrict__ out) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -150,6 +186,236 @@ __global__ __launch_bounds__(256) void k_wave(const uint8_t* __restrict__ base,
         w = wave_sum(w);
         if (lane == 0) out[p] = finish(d.start_sum, w);
     }
+}
+
+
+// ----------------------------------------------- k_stream (the default path) --
+//
+// One wavefront per packet, persistent.  Wave w owns the contiguous packet
+// range [w*per_wave, (w+1)*per_wave) and streams through it with a ring of U
+// outstanding 1 KiB wave-loads (64 lanes x 16 B, nontemporal), so a wave keeps
+// ~U KiB in flight across packet boundaries: the next packet's loads are issued
+// before the current packet is reduced.  Each wave-load covers 16-B chunks
+// [c, c+64) of one packet; the packet's last wave-load triggers the DPP
+// reduction and the fold; results gather in lane (p - g) of a register and
+// leave as one 128-B store per 64 packets.
+//
+// Addressing: a buffer resource per packet whose base is the packet's first
+// byte (any byte alignment; gfx950 buffer loads accept it) and whose
+// num_records is len rounded up to 4.  gfx950 range-checks raw buffer loads per
+// dword (dword k is returned iff 4k+4 <= num_records, else 0; scripts/lab_oob.py),
+// so lanes past the packet read zeros with no select and no memory access, the
+// u16 words are packet-relative (no odd-address byte swap), and the only fix-up
+// is the 1-3 byte tail of a length that is not a multiple of 4, in one lane.
+//
+// Wait-count discipline (what keeps U loads in flight): ring loads are issued
+// from inline asm, exactly one per slot (slots past the range use
+// num_records = 0), and retired by ring_wait<U-1>; hipcc's own wait-count pass
+// cannot follow a ring across the loop back edge and would drain it.
+// Descriptors arrive 64 at a time in per-wave LDS windows by LDS-DMA (also asm,
+// so hipcc does not drain the ring before each LDS read); a window is refilled
+// 64 packets (>= 64 ring loads) before it is read, so the ring's waits retire it.
+
+constexpr int SW_WAVES = 4;  // waves per 256-thread workgroup
+constexpr uint32_t SRD_WORD3 = 0x00020000u;  // raw 32-bit buffer, as make_buffer_rsrc
+
+__device__ __forceinline__ u32x4 buffer_load_nt_asm(uint32_t voff, const u32x4 srd) {
+    // The resource must sit in SGPRs; it is wave-uniform by construction, which
+    // readfirstlane makes explicit to the compiler (cdna_hip_programming.md T20).
+    u32x4 s;
+    s.x = (uint32_t)__builtin_amdgcn_readfirstlane((int)srd.x);
+    s.y = (uint32_t)__builtin_amdgcn_readfirstlane((int)srd.y);
+    s.z = (uint32_t)__builtin_amdgcn_readfirstlane((int)srd.z);
+    s.w = (uint32_t)__builtin_amdgcn_readfirstlane((int)srd.w);
+    // s_nop 4: the resource words may have just been written by v_readfirstlane
+    // (a VALU write of SGPRs); a VMEM read of such SGPRs needs 5 wait states on
+    // gfx9-family parts, and hipcc inserts no hazard padding around inline asm.
+    u32x4 r;
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen nt"
+                 : "=v"(r)
+                 : "v"(voff), "s"(s));
+    return r;
+}
+
+// Sum of the two u16 halves of x, added to acc (v_dot2_u32_u16 with {1,1}).
+__device__ __forceinline__ uint32_t dot2_acc(uint32_t x, uint32_t acc) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 one = {1, 1};
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, x), one, acc, false);
+}
+
+// Issued from asm so hipcc does not see an LDS-DMA in flight.
+__device__ __forceinline__ void fetch_window(const lvlip_csum_desc* __restrict__ descs,
+                                             uint32_t first, uint32_t n, uint32_t lane,
+                                             uint4* win /* LDS, 64 entries */) {
+    uint32_t i = first + lane;
+    i = i < n ? i : n - 1u;  // lanes past the batch re-read a valid descriptor
+    const lvlip_csum_desc* g = descs + i;
+    const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)win);
+    // m0 is reserved to the compiler, which warns on the clobber; nothing else in
+    // these kernels reads m0 (tests/test_isa.py checks every m0 write is ours).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    // s_nop 4: `lds` comes from v_readfirstlane (VALU->SGPR->use hazard) and an
+    // M0 write needs a wait state before an LDS-DMA reads it.
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :
+                 : "v"(g), "s"(lds)
+                 : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
+__device__ __forceinline__ u32x4 window_desc(const uint4* win, uint32_t k) {
+    const uint4 d = win[k];  // uniform address: LDS broadcast
+    u32x4 r;
+    r.x = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.x);
+    r.y = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.y);
+    r.z = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.z);
+    r.w = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.w);
+    return r;
+}
+
+struct PacketMeta {
+    u32x4 srd;        // buffer resource: base = first byte, num_records = round_up(len, 4)
+    uint32_t nch1;    // 16-B chunks, at least 1 (an empty packet still takes one slot)
+    uint32_t lc;      // index of the chunk holding the last byte
+    uint32_t tmask;   // byte mask of the last dword when len % 4 != 0, else 0
+    uint32_t tk;      // dword (0..3) of chunk lc that holds the last byte
+    uint32_t start;   // start_sum
+};
+
+// d = {offset_lo, offset_hi, len, start_sum} (struct lvlip_csum_desc as dwords)
+__device__ __forceinline__ PacketMeta packet_meta(const uint8_t* base, const u32x4 d) {
+    PacketMeta m;
+    const uint64_t a = reinterpret_cast<uint64_t>(base) + (((uint64_t)d.y << 32) | d.x);
+    const int32_t len = (int32_t)d.z;
+    m.srd.x = (uint32_t)a;
+    m.srd.y = (uint32_t)(a >> 32) & 0xffffu;  // stride 0
+    m.srd.w = SRD_WORD3;
+    m.start = d.w;
+    if (len > 0) {
+        const uint32_t l = (uint32_t)len;
+        m.srd.z = (l + 3u) & ~3u;
+        m.nch1 = (l + 15u) >> 4;
+        m.lc = (l - 1u) >> 4;
+        m.tk = ((l - 1u) >> 2) & 3u;
+        m.tmask = (l & 3u) ? ((1u << (8u * (l & 3u))) - 1u) : 0u;
+    } else {
+        m.srd.z = 0;
+        m.nch1 = 1;
+        m.lc = 0;
+        m.tk = 0;
+        m.tmask = 0;
+    }
+    return m;
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base,
+                                                const lvlip_csum_desc* __restrict__ descs,
+                                                uint32_t n, uint32_t per_wave,
+                                                uint16_t* __restrict__ out) {
+    __shared__ uint4 s_win[SW_WAVES][2][64];
+    constexpr uint32_t END = 0xffffffffu;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lane16 = lane * 16u;
+    const uint32_t wid = uniform(threadIdx.x >> 6);
+    const uint32_t wave = uniform(blockIdx.x * SW_WAVES + wid);
+    const uint64_t lo64 = (uint64_t)wave * per_wave;
+    if (lo64 >= n) return;
+    const uint32_t p_lo = (uint32_t)lo64;
+    const uint32_t p_hi = (uint32_t)min<uint64_t>(lo64 + per_wave, (uint64_t)n);
+
+    // descriptor windows: packets [p_lo + 64w, p_lo + 64w + 64) live in s_win[wid][w & 1]
+    fetch_window(descs, p_lo, n, lane, s_win[wid][0]);
+    fetch_window(descs, p_lo + 64u, n, lane, s_win[wid][1]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // issue cursor: packet ip, chunk ic
+    uint32_t ip = p_lo, ic = 0;
+    PacketMeta cur = packet_meta(base, window_desc(s_win[wid][0], 0));
+
+    // consume side
+    uint32_t gc = p_lo;  // results of packets [gc, gc+64) gather in `res`
+    uint32_t res = 0;
+    uint32_t acc = 0;
+
+    u32x4 v[U];
+    uint32_t s_pkt[U], s_start[U], s_last[U], s_tmask[U], s_tpos[U];
+
+    auto issue = [&](int u) {
+        const bool live = ip < p_hi;  // uniform
+        u32x4 srd = cur.srd;
+        if (!live) srd.z = 0;  // past the range: every dword out of range -> zeros
+        v[u] = buffer_load_nt_asm(lane16 + (ic << 4), srd);
+        const bool last = ic + 64u >= cur.nch1;
+        s_pkt[u] = live ? ip : END;
+        s_start[u] = cur.start;
+        s_last[u] = last;
+        s_tmask[u] = last ? cur.tmask : 0u;
+        s_tpos[u] = (cur.lc - ic) | (cur.tk << 8);
+        if (live) {
+            if (!last) {
+                ic += 64u;
+            } else {
+                ++ip;
+                ic = 0;
+                if (ip < p_hi) {
+                    const uint32_t k = ip - p_lo;
+                    if ((k & 63u) == 0u && k >= 64u)  // entered window k/64: refill the other
+                        fetch_window(descs, ip + 64u, n, lane, s_win[wid][((k >> 6) + 1u) & 1u]);
+                    cur = packet_meta(base, window_desc(s_win[wid][(k >> 6) & 1u], k & 63u));
+                }
+            }
+        }
+    };
+
+    auto consume = [&](int u) {
+        // Slot u is the oldest ring load: U-1 ring loads (and possibly result
+        // stores / window DMAs, which only make this wait stricter) came after it.
+        ring_wait<U - 1>(v[u]);
+        u32x4 x = v[u];
+        if (s_tmask[u] != 0u) {  // uniform: zero the bytes past len in the last dword
+            const bool me = lane == (s_tpos[u] & 0xffu);
+            const uint32_t tk = s_tpos[u] >> 8;
+            const uint32_t m = s_tmask[u];
+            x.x &= (me && tk == 0u) ? m : ~0u;
+            x.y &= (me && tk == 1u) ? m : ~0u;
+            x.z &= (me && tk == 2u) ? m : ~0u;
+            x.w &= (me && tk == 3u) ? m : ~0u;
+        }
+        acc = dot2_acc(x.x, acc);
+        acc = dot2_acc(x.y, acc);
+        acc = dot2_acc(x.z, acc);
+        acc = dot2_acc(x.w, acc);
+        if (s_last[u]) {
+            const uint32_t w = wave_sum_dpp(acc);
+            acc = 0;
+            const uint32_t k = s_pkt[u] - gc;
+            if (lane == k) res = finish(s_start[u], w);
+            if (k == 63u || s_pkt[u] + 1u == p_hi) {
+                if (lane <= k) out[gc + lane] = (uint16_t)res;
+                gc += 64u;
+            }
+        }
+    };
+
+#pragma unroll
+    for (int u = 0; u < U; ++u) issue(u);
+    bool done = false;
+    while (!done) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (s_pkt[u] == END) {
+                done = true;
+                break;
+            }
+            consume(u);
+            issue(u);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this wave left in flight
 }
 
 // ------------------------------------------------- k_wave_lds (LDS-DMA path) --
@@ -343,24 +609,6 @@ __global__ __launch_bounds__(FLAT_T) void k_flat(const uint8_t* __restrict__ bas
     if (i_me < n) out[i_me] = finish(start_sum, s_acc[tid]);
 }
 
-// ------------------------------------------------- roofline probe (diagnostic) --
-// Pure streaming read of `bytes` (multiple of 16) — the achievable HBM read rate
-// on this device, measured beside the checksum kernels (bench.py diagnostics).
-__global__ __launch_bounds__(256) void k_read_probe(const uint4* __restrict__ src, uint64_t n16,
-                                                    uint32_t* __restrict__ sink) {
-    uint32_t acc = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        acc += chunk_words<false>(a) + chunk_words<false>(b) + chunk_words<false>(c) +
-               chunk_words<false>(d);
-    }
-    for (; i < n16; i += stride) acc += chunk_words<false>(src[i]);
-    acc = wave_sum(acc);
-    if ((threadIdx.x & 63u) == 0) atomicAdd(sink, acc);
-}
-
 }  // namespace lvlip
 
 // ======================================================== host side (C ABI) ==
@@ -403,10 +651,26 @@ uint32_t grid_for(uint32_t n, uint32_t packets_per_block, int waves_per_cu, int 
 }
 
 template <int U>
-void launch_wave(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
-                 uint32_t n, uint16_t* out) {
-    hipLaunchKernelGGL(lvlip::k_wave<U>, dim3(grid), dim3(256), 0, s,
+void launch_wave_simple(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                        uint32_t n, uint16_t* out) {
+    hipLaunchKernelGGL(lvlip::k_wave_simple<U>, dim3(grid), dim3(256), 0, s,
                        (const uint8_t*)base, d, n, out);
+}
+
+// Persistent streaming launch: waves_per_cu waves on every CU, each owning a
+// contiguous range of ceil(n / waves) packets.
+template <int U>
+void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                   uint32_t n, uint16_t* out) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    uint64_t waves = (uint64_t)cu_count(dev) * (uint64_t)waves_per_cu;
+    if (waves > n) waves = n;
+    waves = (waves + 3) & ~3ull;  // whole 256-thread blocks
+    const uint32_t per_wave = (uint32_t)(((uint64_t)n + waves - 1) / waves);
+    const uint32_t grid = (uint32_t)(waves / 4);
+    hipLaunchKernelGGL(lvlip::k_stream<U>, dim3(grid), dim3(256), 0, s,
+                       (const uint8_t*)base, d, n, per_wave, out);
 }
 
 template <int U>
@@ -455,13 +719,23 @@ int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint
     switch (kernel) {
         case LVLIP_KERNEL_AUTO:
         case LVLIP_KERNEL_WAVE: {
+            if (unroll <= 0) unroll = 4;
+            const int w = wpc > 0 ? wpc : 8;
+            switch (unroll) {
+                case 2: launch_stream<2>(w, s, base, descs, n, out); break;
+                case 4: launch_stream<4>(w, s, base, descs, n, out); break;
+                case 8: launch_stream<8>(w, s, base, descs, n, out); break;
+                default: return LVLIP_EINVAL;
+            }
+            break;
+        }
+        case LVLIP_KERNEL_WAVE_SIMPLE: {
             if (unroll <= 0) unroll = 2;
             const uint32_t grid = grid_for(n, 4, wpc, 4);
             switch (unroll) {
-                case 1: launch_wave<1>(grid, s, base, descs, n, out); break;
-                case 2: launch_wave<2>(grid, s, base, descs, n, out); break;
-                case 4: launch_wave<4>(grid, s, base, descs, n, out); break;
-                case 8: launch_wave<8>(grid, s, base, descs, n, out); break;
+                case 1: launch_wave_simple<1>(grid, s, base, descs, n, out); break;
+                case 2: launch_wave_simple<2>(grid, s, base, descs, n, out); break;
+                case 4: launch_wave_simple<4>(grid, s, base, descs, n, out); break;
                 default: return LVLIP_EINVAL;
             }
             break;
@@ -493,21 +767,6 @@ int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint
 int lvlip_csum_batch_dev(const void* base, const lvlip_csum_desc* descs, uint32_t n,
                          uint16_t* out, void* stream) {
     return lvlip_csum_batch_dev_ex(base, descs, n, out, stream, nullptr);
-}
-
-// Diagnostic: streaming-read probe over `bytes` of device memory (multiple of 16).
-int lvlip_diag_read_probe(const void* src, uint64_t bytes, uint32_t* sink, int waves_per_cu,
-                          void* stream) {
-    if (!src || !sink || (bytes & 15u) || ((uintptr_t)src & 15u)) return LVLIP_EINVAL;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const int wpc = waves_per_cu > 0 ? waves_per_cu : 32;
-    const uint32_t grid = (uint32_t)((uint64_t)cu_count(dev) * wpc / 4);
-    hipLaunchKernelGGL(lvlip::k_read_probe, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       (const uint4*)src, bytes / 16, sink);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "probe launch");
-    return LVLIP_OK;
 }
 
 }  // extern "C"

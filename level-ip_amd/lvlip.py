@@ -24,12 +24,13 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liblvlip_csum.so")
 TESTKIT_PATH = os.path.join(HERE, "liblvlip_testkit.so")
+LAB_PATH = os.path.join(HERE, "liblvlip_lab.so")
 
 # error codes (include/lvlip_csum.h)
 OK, EINVAL, ENODEV, EHIP, ENOMEM, ERANGE = 0, -1, -2, -3, -4, -5
-KERNEL_AUTO, KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_FLAT = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_FLAT, KERNEL_WAVE_SIMPLE = 0, 1, 2, 3, 4
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "wave_lds": KERNEL_WAVE_LDS,
-                "flat": KERNEL_FLAT}
+                "flat": KERNEL_FLAT, "wave_simple": KERNEL_WAVE_SIMPLE}
 
 # struct lvlip_csum_desc {u64 offset; i32 len; u32 start_sum;}  (16 B)
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<i4"), ("start_sum", "<u4")])
@@ -63,6 +64,24 @@ class Iov(ctypes.Structure):
     _fields_ = [("ptr", ctypes.c_void_p), ("len", ctypes.c_int32), ("start_sum", ctypes.c_uint32)]
 
 
+def _share_torch_hip_runtime() -> None:
+    """Make this process use ONE HIP runtime.
+
+    PyTorch-ROCm ships its own libamdhip64.so (SONAME libamdhip64.so.7) and its
+    libtorch_hip.so asks for it by the name "libamdhip64.so".  If our library were
+    loaded first, the dynamic linker would resolve its libamdhip64.so.7 from
+    /opt/rocm and torch would later map a second runtime next to it.  Preloading
+    torch's copy (RTLD_GLOBAL) makes both resolve to the same file."""
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    cand = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
+
+
 def _load(path: str) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise LvlipUnavailable(
@@ -73,6 +92,7 @@ def _load(path: str) -> ctypes.CDLL:
         raise LvlipUnavailable(f"cannot load {path}: {e}") from e
 
 
+_share_torch_hip_runtime()
 _lib = _load(LIB_PATH)
 
 # every entry point declared in include/lvlip_csum.h, with its ctypes signature
@@ -98,8 +118,6 @@ SIGNATURES = {
     "lvlip_abi_version": (ctypes.c_int, []),
     "lvlip_device_count": (ctypes.c_int, []),
     "lvlip_last_hip_error": (ctypes.c_char_p, []),
-    "lvlip_diag_read_probe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
-                                             ctypes.c_int, ctypes.c_void_p]),
 }
 for _name, (_res, _args) in SIGNATURES.items():
     _fn = getattr(_lib, _name)
@@ -195,12 +213,6 @@ def batch_torch(base, descs, out=None, kernel: int = KERNEL_AUTO, unroll: int = 
     return out
 
 
-def read_probe(src_ptr: int, nbytes: int, sink_ptr: int, waves_per_cu: int = 0,
-               stream: int = 0) -> None:
-    _check(_lib.lvlip_diag_read_probe(src_ptr, nbytes, sink_ptr, waves_per_cu, stream or None),
-           "lvlip_diag_read_probe")
-
-
 def device_count() -> int:
     return int(_lib.lvlip_device_count())
 
@@ -274,3 +286,19 @@ def testkit() -> ctypes.CDLL:
                                            ctypes.c_uint32, ctypes.c_void_p]
         _testkit = tk
     return _testkit
+
+
+_lab = None
+
+
+def lab() -> ctypes.CDLL:
+    """liblvlip_lab.so: read-bandwidth probes (diagnostics only)."""
+    global _lab
+    if _lab is None:
+        lb = _load(LAB_PATH)
+        lb.lvlip_lab_probe.restype = ctypes.c_int
+        lb.lvlip_lab_probe.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_void_p]
+        _lab = lb
+    return _lab

@@ -24,11 +24,14 @@ THREADS = min(16, os.cpu_count() or 1)
 # (kernel, unroll, waves_per_cu)
 VARIANTS = [
     (lvlip.KERNEL_AUTO, 0, 0),
-    (lvlip.KERNEL_WAVE, 1, 0),
-    (lvlip.KERNEL_WAVE, 2, 0),
+    (lvlip.KERNEL_WAVE, 2, 0),     # persistent stream, ring depth 2/4/8
     (lvlip.KERNEL_WAVE, 4, 0),
     (lvlip.KERNEL_WAVE, 8, 0),
-    (lvlip.KERNEL_WAVE, 2, 16),   # persistent grid-stride form
+    (lvlip.KERNEL_WAVE, 4, 1),     # 1 wave/CU: long per-wave ranges, window refills
+    (lvlip.KERNEL_WAVE, 4, 16),
+    (lvlip.KERNEL_WAVE_SIMPLE, 1, 0),
+    (lvlip.KERNEL_WAVE_SIMPLE, 2, 0),
+    (lvlip.KERNEL_WAVE_SIMPLE, 4, 8),
     (lvlip.KERNEL_WAVE_LDS, 1, 0),
     (lvlip.KERNEL_WAVE_LDS, 2, 0),
     (lvlip.KERNEL_WAVE_LDS, 4, 8),
@@ -194,7 +197,8 @@ def test_full_size_bit_exact(name):
     bad = np.nonzero(got_auto != want)[0]
     assert bad.size == 0, f"{bad.size} of {b.n} differ; first {bad[:5]}"
     # size-independent property: every kernel variant agrees, and reruns are identical
-    for variant in [(lvlip.KERNEL_WAVE, 4, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
+    for variant in [(lvlip.KERNEL_WAVE, 4, 0), (lvlip.KERNEL_WAVE, 8, 4),
+                    (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_AUTO, 0, 0)]:
         assert np.array_equal(run(base, descs, variant, out), want), variant
     # adversarial packets really are there and fold as the reference does
@@ -256,11 +260,14 @@ def test_host_flat_config_slices():
         assert np.array_equal(ctx.batch_host_flat(host, b.descs), want)
 
 
-def test_read_probe_sums():
+def test_lab_read_probe_sums():
+    lab = lvlip.lab()
     a = torch.arange(0, 1 << 20, dtype=torch.int32, device="cuda")
-    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
-    lvlip.read_probe(a.data_ptr(), a.numel() * 4, sink.data_ptr(), 8,
-                     torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
     h = a.cpu().numpy().view(np.uint16).astype(np.uint64).sum() & 0xFFFFFFFF
-    assert int(sink.item()) & 0xFFFFFFFF == int(h)
+    for mode, unroll, nt in [(0, 4, 0), (1, 4, 1), (2, 2, 0), (3, 2, 0)]:
+        sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+        rc = lab.lvlip_lab_probe(a.data_ptr(), a.numel() * 4, sink.data_ptr(), mode, unroll, nt,
+                                 64, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert int(sink.item()) & 0xFFFFFFFF == int(h), (mode, unroll, nt)

@@ -1,0 +1,103 @@
+"""ISA guards for the stream kernel (CPU-only: hipcc cross-compiles gfx950).
+
+The stream kernel relies on hand-placed inline asm (csum_kernels.hip, k_stream):
+  * buffer_load_dwordx4 whose resource words come from v_readfirstlane, a VALU
+    write of SGPRs: a VMEM read of them needs 5 wait states (s_nop 4), which
+    hipcc does not insert around inline asm;
+  * an LDS-DMA whose M0 is written just before it (needs a wait state);
+  * a ring of U loads retired by vmcnt(U-1): hipcc must not add draining waits.
+These checks read the generated assembly and fail if any of that regresses.
+"""
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "level-ip_amd", "csrc", "csum_kernels.hip")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.fixture(scope="module")
+def asm():
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "k.s")
+        subprocess.run([HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17",
+                        "-I" + os.path.join(ROOT, "include"), "-S", "--cuda-device-only",
+                        SRC, "-o", out], check=True, capture_output=True)
+        return open(out).read()
+
+
+def functions(text):
+    """name -> list of instruction lines (comments/labels/directives dropped)."""
+    funcs, cur, name = {}, None, None
+    for line in text.splitlines():
+        m = re.match(r"^(_Z\w+):", line)
+        if m:
+            name, cur = m.group(1), []
+            funcs[name] = cur
+            continue
+        if cur is None:
+            continue
+        s = line.split(";")[0].strip()
+        if not s or s.startswith(".") or s.endswith(":"):
+            if "s_endpgm" in line:
+                cur = None
+            continue
+        cur.append(s)
+        if s.startswith("s_endpgm"):
+            cur = None
+    return funcs
+
+
+def stream_kernels(asm):
+    f = functions(asm)
+    ks = {n: body for n, body in f.items() if "k_stream" in n}
+    assert ks, "no k_stream instantiations found"
+    return ks
+
+
+def test_buffer_loads_padded_against_valu_sgpr_hazard(asm):
+    for name, body in stream_kernels(asm).items():
+        n = 0
+        for i, ins in enumerate(body):
+            if ins.startswith("buffer_load_dwordx4") and ins.endswith("offen nt"):
+                n += 1
+                assert body[i - 1] == "s_nop 4", (name, i, body[i - 3:i + 1])
+        assert n >= 2, name
+
+
+def test_lds_dma_m0_sequence(asm):
+    for name, body in stream_kernels(asm).items():
+        n = 0
+        for i, ins in enumerate(body):
+            if ins.startswith("global_load_lds_dwordx4"):
+                n += 1
+                assert body[i - 1] == "s_nop 0", (name, body[i - 3:i + 1])
+                assert body[i - 2].startswith("s_mov_b32 m0,"), (name, body[i - 3:i + 1])
+                assert body[i - 3] == "s_nop 4", (name, body[i - 4:i + 1])
+            elif "m0" in re.split(r"[\s,]+", ins):
+                assert ins.startswith("s_mov_b32 m0,") and body[i + 2].startswith(
+                    "global_load_lds"), (name, ins)
+        assert n >= 2, name
+
+
+def test_ring_waits_are_counted_not_draining(asm):
+    for name, body in stream_kernels(asm).items():
+        u = int(re.search(r"k_streamILi(\d+)E", name).group(1))
+        waits = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt" in ins]
+        ring = [w for w in waits if f"vmcnt({u - 1})" in w]
+        drains = [w for w in waits if "vmcnt(0)" in w]
+        assert len(ring) == u, (name, waits)
+        # one drain after the first window fill, one before s_endpgm
+        assert len(drains) <= 2, (name, waits)
+
+
+def test_no_scratch(asm):
+    for m in re.finditer(r"\.name:\s+(_Z\w*k_stream\w*)\n(?:.*\n){0,60}?\s+\.private_segment_fixed_size:\s+(\d+)",
+                         asm):
+        assert int(m.group(2)) == 0, m.group(1)
