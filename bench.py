@@ -46,8 +46,8 @@ WORKLOAD_TEXT = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--workload", default="tcp1500", choices=sorted(WORKLOAD_TEXT))
     p.add_argument("--n", type=int, default=None, help="packets (frames for mixed) per rank")
     p.add_argument("--kernel", default="auto",
@@ -259,8 +259,8 @@ def timed(torch, fn, stream, reps=20, warm=3):
 
 def sweep(lvlip, torch, base, descs, out, b, stream):
     res = {}
-    variants = [("wave", 2, 8), ("wave", 4, 4), ("wave", 4, 8), ("wave", 4, 16), ("wave", 8, 4),
-                ("wave", 8, 8), ("wave_simple", 2, 0), ("wave_lds", 2, 0), ("flat", 0, 0)]
+    variants = [("wave", 2, 8), ("wave", 2, 12), ("wave", 2, 16), ("wave", 3, 12), ("wave", 3, 16),
+                ("wave", 4, 16), ("wave_simple", 2, 0), ("wave_lds", 2, 0), ("flat", 0, 0)]
     for rnd in range(2):  # interleaved rounds in one process
         for k, u, w in variants:
             def f():

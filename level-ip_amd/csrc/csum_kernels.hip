@@ -109,17 +109,6 @@ __device__ __forceinline__ uint4 load_nt(const uint8_t* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// Wait until at most N vector-memory operations are outstanding.  The slot's
-// register is an in/out operand, so no instruction that reads it can be
-// scheduled above the wait (a plain asm barrier does not order register-only
-// instructions, cdna_hip_programming.md §5.4 rule 18).
-template <int N>
-__device__ __forceinline__ void ring_wait(u32x4& r) {
-    // "memory": LDS reads of descriptor windows (retired by these same waits)
-    // must not move above it either.
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r) : "n"(N) : "memory");
-}
-
 // utils.c:46-54.  Two unconditional folds equal the reference's while loop:
 // after the first T <= 0x1fffe, after the second T <= 0xffff, and a fold of a
 // value <= 0xffff is the identity.
@@ -192,13 +181,12 @@ __global__ __launch_bounds__(256) void k_wave_simple(const uint8_t* __restrict__
 // ----------------------------------------------- k_stream (the default path) --
 //
 // One wavefront per packet, persistent.  Wave w owns the contiguous packet
-// range [w*per_wave, (w+1)*per_wave) and streams through it with a ring of U
-// outstanding 1 KiB wave-loads (64 lanes x 16 B, nontemporal), so a wave keeps
-// ~U KiB in flight across packet boundaries: the next packet's loads are issued
-// before the current packet is reduced.  Each wave-load covers 16-B chunks
-// [c, c+64) of one packet; the packet's last wave-load triggers the DPP
-// reduction and the fold; results gather in lane (p - g) of a register and
-// leave as one 128-B store per 64 packets.
+// range [w*per_wave, (w+1)*per_wave) and streams through it with a ring of R
+// outstanding pieces; a piece is up to 2 KiB of one packet, read as two 1 KiB
+// wave-loads (64 lanes x 16 B, nontemporal).  The next packet's loads are
+// issued before the current packet is reduced.  The packet's last piece
+// triggers the DPP reduction and the fold; results gather in lane (p - g) of a
+// register and leave as one 128-B store per 64 packets.
 //
 // Addressing: a buffer resource per packet whose base is the packet's first
 // byte (any byte alignment; gfx950 buffer loads accept it) and whose
@@ -208,10 +196,10 @@ __global__ __launch_bounds__(256) void k_wave_simple(const uint8_t* __restrict__
 // u16 words are packet-relative (no odd-address byte swap), and the only fix-up
 // is the 1-3 byte tail of a length that is not a multiple of 4, in one lane.
 //
-// Wait-count discipline (what keeps U loads in flight): ring loads are issued
-// from inline asm, exactly one per slot (slots past the range use
-// num_records = 0), and retired by ring_wait<U-1>; hipcc's own wait-count pass
-// cannot follow a ring across the loop back edge and would drain it.
+// Wait-count discipline (what keeps the ring in flight): ring loads are issued
+// from inline asm, exactly two per piece (pieces past the range use
+// num_records = 0), and retired by piece_wait<2(R-1)>; hipcc's own wait-count
+// pass cannot follow a ring across the loop back edge and would drain it.
 // Descriptors arrive 64 at a time in per-wave LDS windows by LDS-DMA (also asm,
 // so hipcc does not drain the ring before each LDS read); a window is refilled
 // 64 packets (>= 64 ring loads) before it is read, so the ring's waits retire it.
@@ -278,10 +266,8 @@ __device__ __forceinline__ u32x4 window_desc(const uint4* win, uint32_t k) {
 
 struct PacketMeta {
     u32x4 srd;        // buffer resource: base = first byte, num_records = round_up(len, 4)
-    uint32_t nch1;    // 16-B chunks, at least 1 (an empty packet still takes one slot)
-    uint32_t lc;      // index of the chunk holding the last byte
-    uint32_t tmask;   // byte mask of the last dword when len % 4 != 0, else 0
-    uint32_t tk;      // dword (0..3) of chunk lc that holds the last byte
+    uint32_t tinfo;   // lc << 4 | tk << 2 | (len & 3): lc = chunk holding the last byte
+                      // (0 for empty packets, which still take one slot), tk = its dword
     uint32_t start;   // start_sum
 };
 
@@ -290,34 +276,38 @@ __device__ __forceinline__ PacketMeta packet_meta(const uint8_t* base, const u32
     PacketMeta m;
     const uint64_t a = reinterpret_cast<uint64_t>(base) + (((uint64_t)d.y << 32) | d.x);
     const int32_t len = (int32_t)d.z;
+    const uint32_t l = len > 0 ? (uint32_t)len : 0u;
+    const uint32_t lm1 = l ? l - 1u : 0u;
     m.srd.x = (uint32_t)a;
     m.srd.y = (uint32_t)(a >> 32) & 0xffffu;  // stride 0
+    m.srd.z = (l + 3u) & ~3u;                 // 0 for empty packets: all dwords zero
     m.srd.w = SRD_WORD3;
+    m.tinfo = ((lm1 >> 4) << 4) | (((lm1 >> 2) & 3u) << 2) | (l & 3u);
     m.start = d.w;
-    if (len > 0) {
-        const uint32_t l = (uint32_t)len;
-        m.srd.z = (l + 3u) & ~3u;
-        m.nch1 = (l + 15u) >> 4;
-        m.lc = (l - 1u) >> 4;
-        m.tk = ((l - 1u) >> 2) & 3u;
-        m.tmask = (l & 3u) ? ((1u << (8u * (l & 3u))) - 1u) : 0u;
-    } else {
-        m.srd.z = 0;
-        m.nch1 = 1;
-        m.lc = 0;
-        m.tk = 0;
-        m.tmask = 0;
-    }
     return m;
 }
 
-template <int U>
+// Retire the two loads of a ring piece (both operands are in/out, so nothing
+// that reads them can be scheduled above the wait).
+template <int N>
+__device__ __forceinline__ void piece_wait(u32x4& a, u32x4& b) {
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
+
+// The ring is organised in pieces: a piece is up to 2 KiB of one packet (two
+// 1 KiB wave-loads, always both issued; chunks past the packet read zeros), so
+// all per-piece bookkeeping is amortised over 2 KiB and a 1500-B segment is one
+// piece.  R pieces are in flight; the oldest is retired by vmcnt(2*(R-1)).
+// (r01 profile of a per-1KiB-slot ring: ~130 SALU per packet, the CU's scalar
+// unit ~80 % busy and the kernel SALU-bound; this layout cuts that ~3x.)
+template <int R>
 __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base,
                                                 const lvlip_csum_desc* __restrict__ descs,
                                                 uint32_t n, uint32_t per_wave,
                                                 uint16_t* __restrict__ out) {
     __shared__ uint4 s_win[SW_WAVES][2][64];
     constexpr uint32_t END = 0xffffffffu;
+    constexpr uint32_t PIECE = 2048u;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lane16 = lane * 16u;
     const uint32_t wid = uniform(threadIdx.x >> 6);
@@ -332,8 +322,8 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
     fetch_window(descs, p_lo + 64u, n, lane, s_win[wid][1]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    // issue cursor: packet ip, chunk ic
-    uint32_t ip = p_lo, ic = 0;
+    // issue cursor: packet ip, byte offset io of the next piece in it
+    uint32_t ip = p_lo, io = 0;
     PacketMeta cur = packet_meta(base, window_desc(s_win[wid][0], 0));
 
     // consume side
@@ -341,26 +331,31 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
     uint32_t res = 0;
     uint32_t acc = 0;
 
-    u32x4 v[U];
-    uint32_t s_pkt[U], s_start[U], s_last[U], s_tmask[U], s_tpos[U];
+    u32x4 va[R], vb[R];
+    // per piece: packet (END past the range), start_sum, and
+    // meta = last | (len & 3) << 1 | (byte offset of the last dword in the piece) << 3
+    uint32_t s_pkt[R], s_start[R], s_meta[R];
 
-    auto issue = [&](int u) {
+    auto issue = [&](int r) {
         const bool live = ip < p_hi;  // uniform
         u32x4 srd = cur.srd;
         if (!live) srd.z = 0;  // past the range: every dword out of range -> zeros
-        v[u] = buffer_load_nt_asm(lane16 + (ic << 4), srd);
-        const bool last = ic + 64u >= cur.nch1;
-        s_pkt[u] = live ? ip : END;
-        s_start[u] = cur.start;
-        s_last[u] = last;
-        s_tmask[u] = last ? cur.tmask : 0u;
-        s_tpos[u] = (cur.lc - ic) | (cur.tk << 8);
+        const uint32_t off = lane16 + io;
+        va[r] = buffer_load_nt_asm(off, srd);
+        vb[r] = buffer_load_nt_asm(off + 1024u, srd);
+        // cur.srd.z = round_up(len, 4): the piece is the packet's last when it
+        // reaches that (or the packet is empty)
+        const bool last = io + PIECE >= cur.srd.z;
+        const uint32_t lastdw = (cur.srd.z - 4u) - io;  // last dword, piece-relative
+        s_pkt[r] = live ? ip : END;
+        s_start[r] = cur.start;
+        s_meta[r] = (uint32_t)last | ((cur.tinfo & 3u) << 1) | (lastdw << 3);
         if (live) {
             if (!last) {
-                ic += 64u;
+                io += PIECE;
             } else {
                 ++ip;
-                ic = 0;
+                io = 0;
                 if (ip < p_hi) {
                     const uint32_t k = ip - p_lo;
                     if ((k & 63u) == 0u && k >= 64u)  // entered window k/64: refill the other
@@ -371,30 +366,42 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
         }
     };
 
-    auto consume = [&](int u) {
-        // Slot u is the oldest ring load: U-1 ring loads (and possibly result
-        // stores / window DMAs, which only make this wait stricter) came after it.
-        ring_wait<U - 1>(v[u]);
-        u32x4 x = v[u];
-        if (s_tmask[u] != 0u) {  // uniform: zero the bytes past len in the last dword
-            const bool me = lane == (s_tpos[u] & 0xffu);
-            const uint32_t tk = s_tpos[u] >> 8;
-            const uint32_t m = s_tmask[u];
-            x.x &= (me && tk == 0u) ? m : ~0u;
-            x.y &= (me && tk == 1u) ? m : ~0u;
-            x.z &= (me && tk == 2u) ? m : ~0u;
-            x.w &= (me && tk == 3u) ? m : ~0u;
+    auto consume = [&](int r) {
+        // Piece r's two loads are the oldest in flight: 2*(R-1) ring loads (and
+        // possibly result stores / window DMAs, which only make this stricter)
+        // were issued after them.
+        piece_wait<2 * (R - 1)>(va[r], vb[r]);
+        u32x4 x = va[r], y = vb[r];
+        const uint32_t meta = s_meta[r];
+        const uint32_t len3 = (meta >> 1) & 3u;
+        if ((meta & 1u) && len3) {  // uniform: keep bytes [0, len & 3) of the last dword
+            const uint32_t pos = meta >> 3;  // byte offset of that dword in the piece
+            const uint32_t m = (1u << (8u * len3)) - 1u;
+            const bool me = lane == ((pos >> 4) & 63u);
+            const uint32_t tk = (pos >> 2) & 3u;
+            const bool in_b = pos >= 1024u;
+            const uint32_t m0 = (me && tk == 0u) ? m : ~0u, m1 = (me && tk == 1u) ? m : ~0u;
+            const uint32_t m2 = (me && tk == 2u) ? m : ~0u, m3 = (me && tk == 3u) ? m : ~0u;
+            if (in_b) {
+                y.x &= m0; y.y &= m1; y.z &= m2; y.w &= m3;
+            } else {
+                x.x &= m0; x.y &= m1; x.z &= m2; x.w &= m3;
+            }
         }
         acc = dot2_acc(x.x, acc);
         acc = dot2_acc(x.y, acc);
         acc = dot2_acc(x.z, acc);
         acc = dot2_acc(x.w, acc);
-        if (s_last[u]) {
+        acc = dot2_acc(y.x, acc);
+        acc = dot2_acc(y.y, acc);
+        acc = dot2_acc(y.z, acc);
+        acc = dot2_acc(y.w, acc);
+        if (meta & 1u) {
             const uint32_t w = wave_sum_dpp(acc);
             acc = 0;
-            const uint32_t k = s_pkt[u] - gc;
-            if (lane == k) res = finish(s_start[u], w);
-            if (k == 63u || s_pkt[u] + 1u == p_hi) {
+            const uint32_t k = s_pkt[r] - gc;
+            if (lane == k) res = finish(s_start[r], w);
+            if (k == 63u || s_pkt[r] + 1u == p_hi) {
                 if (lane <= k) out[gc + lane] = (uint16_t)res;
                 gc += 64u;
             }
@@ -402,17 +409,17 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
     };
 
 #pragma unroll
-    for (int u = 0; u < U; ++u) issue(u);
+    for (int r = 0; r < R; ++r) issue(r);
     bool done = false;
     while (!done) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (s_pkt[u] == END) {
+        for (int r = 0; r < R; ++r) {
+            if (s_pkt[r] == END) {
                 done = true;
                 break;
             }
-            consume(u);
-            issue(u);
+            consume(r);
+            issue(r);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this wave left in flight
@@ -719,12 +726,13 @@ int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint
     switch (kernel) {
         case LVLIP_KERNEL_AUTO:
         case LVLIP_KERNEL_WAVE: {
-            if (unroll <= 0) unroll = 4;
-            const int w = wpc > 0 ? wpc : 8;
+            // unroll = 2-KiB pieces in flight per wave (2 = up to 4 KiB)
+            if (unroll <= 0) unroll = 2;
+            const int w = wpc > 0 ? wpc : 16;
             switch (unroll) {
                 case 2: launch_stream<2>(w, s, base, descs, n, out); break;
+                case 3: launch_stream<3>(w, s, base, descs, n, out); break;
                 case 4: launch_stream<4>(w, s, base, descs, n, out); break;
-                case 8: launch_stream<8>(w, s, base, descs, n, out); break;
                 default: return LVLIP_EINVAL;
             }
             break;

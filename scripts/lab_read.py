@@ -38,17 +38,19 @@ def main():
     nb = base.numel() & ~1023
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     variants = []
-    for mode in (1, 2):
+    if os.environ.get("LAB_SET") == "csum":
+        variants = [("probe", 1, 8, 1, 2), ("probe", 2, 4, 1, 2)]
+    for mode in (() if os.environ.get("LAB_SET") == "csum" else (1, 2)):
         for u in (4, 8):
             for nt in (0, 1):
                 for bpc in (2, 4, 8):
                     variants.append(("probe", mode, u, nt, bpc))
-    for u in (4, 8):
+    for u in (() if os.environ.get("LAB_SET") == "csum" else (4, 8)):
         for bpc in (2, 4):
             variants.append(("probe", 3, u, 0, bpc))
     ck = [("csum", k, u, w) for k, u, w in [
-        ("wave", 2, 8), ("wave", 4, 4), ("wave", 4, 8), ("wave", 4, 12), ("wave", 4, 16),
-        ("wave", 8, 4), ("wave", 8, 8), ("wave", 8, 16), ("wave", 2, 16),
+        ("wave", 2, 4), ("wave", 2, 8), ("wave", 2, 12), ("wave", 2, 16), ("wave", 2, 24),
+        ("wave", 3, 8), ("wave", 3, 12), ("wave", 3, 16), ("wave", 4, 8), ("wave", 4, 16),
         ("wave_simple", 2, 0), ("wave_lds", 2, 0), ("flat", 0, 0)]]
     res = {}
     for rnd in range(3):

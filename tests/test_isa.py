@@ -5,7 +5,8 @@ The stream kernel relies on hand-placed inline asm (csum_kernels.hip, k_stream):
     write of SGPRs: a VMEM read of them needs 5 wait states (s_nop 4), which
     hipcc does not insert around inline asm;
   * an LDS-DMA whose M0 is written just before it (needs a wait state);
-  * a ring of U loads retired by vmcnt(U-1): hipcc must not add draining waits.
+  * a ring of R two-load pieces retired by vmcnt(2(R-1)): hipcc must not add
+    draining waits.
 These checks read the generated assembly and fail if any of that regresses.
 """
 import os
@@ -88,11 +89,11 @@ def test_lds_dma_m0_sequence(asm):
 
 def test_ring_waits_are_counted_not_draining(asm):
     for name, body in stream_kernels(asm).items():
-        u = int(re.search(r"k_streamILi(\d+)E", name).group(1))
+        r = int(re.search(r"k_streamILi(\d+)E", name).group(1))  # pieces in flight
         waits = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt" in ins]
-        ring = [w for w in waits if f"vmcnt({u - 1})" in w]
+        ring = [w for w in waits if f"vmcnt({2 * (r - 1)})" in w]
         drains = [w for w in waits if "vmcnt(0)" in w]
-        assert len(ring) == u, (name, waits)
+        assert len(ring) == r, (name, waits)
         # one drain after the first window fill, one before s_endpgm
         assert len(drains) <= 2, (name, waits)
 
