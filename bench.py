@@ -155,11 +155,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    # RCCL (backend "nccl") on the 8-GPU node; LVLIP_DIST_BACKEND=gloo rehearses the
+    # N>1 code path with several ranks on one GPU (device = local rank mod count).
+    backend = os.environ.get("LVLIP_DIST_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
     if lvlip.device_count() == 0:
         raise SystemExit("bench.py needs a HIP device")
 
@@ -193,14 +199,14 @@ def main():
     if world > 1:
         dist.barrier()
     kern_ms = e0.elapsed_time(e1) / args.steps  # events on the launch stream
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max, kern_ms_max = float(t[0]), float(t[1])
 
     total_bytes = b.algo_bytes * world  # equal shards (uniform), near-equal for mixed
     if world > 1 and args.workload == "mixed":
-        tb = torch.tensor([float(b.algo_bytes)], dtype=torch.float64, device=dev)
+        tb = torch.tensor([float(b.algo_bytes)], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tb)
         total_bytes = float(tb[0])
     value = total_bytes * args.steps / wall_max / 1e9

@@ -1,0 +1,74 @@
+"""Multi-GPU sharding of a checksum batch (one process per GPU).
+
+Packets are independent, so a batch shards by contiguous
+descriptor ranges with no exchange on the data path:
+
+  partition(lens, world)   contiguous ranges balanced by bytes (prefix sums), so
+                           a ragged batch gives every rank about the same HBM
+                           traffic, which is what bounds the kernel
+  local_batch(...)         a rank's descriptors rebased to its own byte span
+  gather_results(...)      results back in batch order (torch.distributed
+                           all_gather: RCCL on GPUs, gloo on CPU tests), the only
+                           collective, 2 bytes per packet
+
+bench.py's weak-scaling run does not move packets at all: each rank
+generates its own shard of the stream (workloads.make(first=rank*n)).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<i4"), ("start_sum", "<u4")])
+
+
+def partition(lens: np.ndarray, world: int) -> list[tuple[int, int]]:
+    """[lo, hi) descriptor ranges, contiguous, covering all n, balanced by bytes.
+
+    Rank r gets the descriptors whose byte prefix falls in
+    [r*T/world, (r+1)*T/world), T = total bytes; empty (len <= 0) descriptors
+    cost nothing and go with their neighbours."""
+    lens = np.maximum(np.asarray(lens, dtype=np.int64), 0)
+    n = lens.size
+    if world <= 1 or n == 0:
+        return [(0, n)] + [(n, n)] * max(0, world - 1)
+    pre = np.concatenate([[0], np.cumsum(lens)])
+    total = int(pre[-1])
+    if total == 0:  # all empty: split by count
+        cuts = [n * r // world for r in range(world + 1)]
+    else:
+        targets = [total * r // world for r in range(world + 1)]
+        cuts = [int(np.searchsorted(pre, t, side="left")) for t in targets]
+        cuts[0], cuts[-1] = 0, n
+        for r in range(1, world + 1):  # monotone
+            cuts[r] = max(cuts[r], cuts[r - 1])
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def local_batch(descs: np.ndarray, lo: int, hi: int) -> tuple[np.ndarray, int, int]:
+    """Descriptors [lo, hi) rebased to their own 16-B aligned byte span.
+
+    Returns (local_descs, span_start, span_bytes): the rank needs bytes
+    [span_start, span_start + span_bytes) of the global buffer."""
+    d = np.ascontiguousarray(descs[lo:hi]).copy()
+    if d.size == 0:
+        return d, 0, 0
+    end = d["offset"] + np.maximum(d["len"], 0).astype(np.uint64)
+    start = int(d["offset"].min()) & ~15
+    stop = (int(end.max()) + 15) & ~15
+    d["offset"] -= np.uint64(start)
+    return d, start, stop - start
+
+
+def gather_results(local_out, counts: list[int], group=None):
+    """All-gather per-rank uint16 result tensors (sizes `counts`) into batch order."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    m = max(counts) if counts else 0
+    # carried as int32 (gloo has no 16-bit integer collectives); bit pattern kept
+    buf = torch.zeros(m, dtype=torch.int32, device=local_out.device)
+    buf[: local_out.numel()] = local_out.view(torch.int16).to(torch.int32) & 0xFFFF
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)]).to(torch.int16)
