@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--workload", default="tcp1500", choices=sorted(WORKLOAD_TEXT))
     p.add_argument("--n", type=int, default=None, help="packets (frames for mixed) per rank")
     p.add_argument("--kernel", default="auto",
-                   choices=["auto", "wave", "wave_lds", "flat", "wave_simple"])
+                   choices=["auto", "wave", "wave_lds", "flat", "wave_simple", "flat_v1"])
     p.add_argument("--unroll", type=int, default=0)
     p.add_argument("--waves-per-cu", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -266,7 +266,8 @@ def timed(torch, fn, stream, reps=20, warm=3):
 def sweep(lvlip, torch, base, descs, out, b, stream):
     res = {}
     variants = [("wave", 2, 8), ("wave", 2, 12), ("wave", 2, 16), ("wave", 3, 12), ("wave", 3, 16),
-                ("wave", 4, 16), ("wave_simple", 2, 0), ("wave_lds", 2, 0), ("flat", 0, 0)]
+                ("wave", 4, 16), ("wave_simple", 2, 0), ("wave_lds", 2, 0), ("flat", 2, 0),
+                ("flat", 4, 0), ("flat", 8, 0), ("flat_v1", 0, 0)]
     for rnd in range(2):  # interleaved rounds in one process
         for k, u, w in variants:
             def f():

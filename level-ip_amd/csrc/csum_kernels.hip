@@ -616,6 +616,235 @@ __global__ __launch_bounds__(FLAT_T) void k_flat(const uint8_t* __restrict__ bas
     if (i_me < n) out[i_me] = finish(start_sum, s_acc[tid]);
 }
 
+
+// ------------------------------------------------- k_flat2 (ragged batches) --
+//
+// Chunk-balanced tile sweep, for batches of many small or mixed-size packets
+// (20-B IPv4 headers next to 64-1460-B payloads, configs[3]).  A 256-thread
+// workgroup owns 256 descriptors.  Phase 1 lays their 16-B aligned chunks end to
+// end in a virtual chunk space (exclusive prefix of chunk counts) and marks each
+// packet's first chunk in a head bitmap, kept per 64-chunk group with the
+// number of heads before the group.  Phase 2 sweeps the chunk space, one group
+// of 64 chunks per wave-load, U groups in flight per wave:
+//   rank   = heads before the group + v_mbcnt(heads below this lane) + own bit - 1
+//            (no search: the packet of every lane in two mbcnt instructions),
+//   bytes  = 16-B aligned loads from the packet's own address (coalesced across
+//            packet boundaries), first/last chunk bytes masked, odd-address
+//            packets byte-swapped within u16 halves (v_perm),
+//   reduce = inclusive DPP prefix sum over the wave; each segment's tail lane
+//            takes P(tail) - P(head-1) and adds it to the packet's u32
+//            accumulator in LDS (mod-2^32 adds: exact in any order).
+// Packets longer than FCAP chunks go to a whole-wave loop instead.
+constexpr int FT = 256;                  // descriptors per tile = threads
+constexpr uint32_t FCAP = 128;           // chunks of the largest swept packet (2 KiB)
+constexpr uint32_t FGROUPS = FT * FCAP / 64;
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_row_shr(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+// inclusive prefix sum over the 64 lanes (u32, wrap-around)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += dpp_row_shr<0x111>(v);  // row_shr:1
+    v += dpp_row_shr<0x112>(v);  // row_shr:2
+    v += dpp_row_shr<0x114>(v);  // row_shr:4
+    v += dpp_row_shr<0x118>(v);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+
+// exclusive prefix over the 256 threads of a workgroup; *total gets the sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp /* >= 4 */,
+                                                    uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane == 63u) s_tmp[wid] = incl;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t t = s_tmp[k];
+        before += (k < wid) ? t : 0u;
+        all += t;
+    }
+    __syncthreads();
+    *total = all;
+    return before + incl - v;
+}
+
+// byte mask of bytes [b0, b1) of a 16-B chunk that fall in dword j
+__device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
+    const int s = min(max(b0 - 4 * j, 0), 4);
+    const int e = min(max(b1 - 4 * j, 0), 4);
+    const int w = (e - s) * 8;
+    if (w <= 0) return 0u;
+    if (w >= 32) return 0xffffffffu;
+    return ((1u << w) - 1u) << (8 * s);
+}
+
+template <int U>
+__global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
+                                              const lvlip_csum_desc* __restrict__ descs,
+                                              uint32_t n, uint16_t* __restrict__ out) {
+    __shared__ uint4 s_rec[FT];        // by rank: {a0 lo, a0 hi, cstart, meta}
+    __shared__ uint4 s_grp[FGROUPS];   // by 64-chunk group: {heads lo, heads hi, heads before, 0}
+    __shared__ uint32_t s_acc[FT];     // by descriptor
+    __shared__ uint32_t s_big[FT];     // descriptors longer than FCAP chunks
+    __shared__ uint32_t s_tmp[8];
+
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t tile0 = blockIdx.x * (uint32_t)FT;
+    const uint32_t t = tid;
+    const uint32_t i_me = tile0 + t;
+
+    // ---- phase 1: descriptors -> chunk counts, ranks, records, head bitmap
+    uint32_t start_sum = 0, nch = 0, meta = 0;
+    uint64_t a0 = 0;
+    bool big = false;
+    if (i_me < n) {
+        const lvlip_csum_desc d = descs[i_me];
+        start_sum = d.start_sum;
+        if (d.len > 0) {
+            const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
+            a0 = abs & ~15ull;
+            const uint32_t lo = (uint32_t)(abs & 15ull);
+            const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
+            const uint64_t c64 = (span + 15u) >> 4;
+            const uint32_t lastv = (uint32_t)(span - 16ull * (c64 - 1u));
+            big = c64 > FCAP;
+            nch = big ? 0u : (uint32_t)c64;
+            meta = lo | (lastv << 4) | ((uint32_t)(abs & 1ull) << 9) |
+                   (((uint32_t)(c64 - 1u) & 127u) << 10) | (t << 18);
+        }
+    }
+    s_acc[t] = 0;
+    for (uint32_t g = t; g < FGROUPS; g += FT) s_grp[g] = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t nbig = 0;
+    const uint32_t big_pos = block_excl_scan(big ? 1u : 0u, s_tmp, &nbig);
+    if (big) s_big[big_pos] = t;
+    uint32_t nsmall = 0;
+    const uint32_t rank = block_excl_scan(nch ? 1u : 0u, s_tmp, &nsmall);
+    uint32_t C = 0;
+    const uint32_t cstart = block_excl_scan(nch, s_tmp, &C);
+    if (nch) {
+        s_rec[rank] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), cstart, meta);
+        const uint32_t g = cstart >> 6, b = cstart & 63u;
+        if (b < 32u) atomicOr(&s_grp[g].x, 1u << b);
+        else atomicOr(&s_grp[g].y, 1u << (b - 32u));
+    }
+    __syncthreads();
+    const uint32_t G = (C + 63u) >> 6;
+    // heads before each group: two groups per thread, block scan of the popcounts
+    {
+        const uint32_t g0 = 2u * t, g1 = 2u * t + 1u;
+        const uint32_t p0 = g0 < G ? (uint32_t)__popcll(((uint64_t)s_grp[g0].y << 32) | s_grp[g0].x) : 0u;
+        const uint32_t p1 = g1 < G ? (uint32_t)__popcll(((uint64_t)s_grp[g1].y << 32) | s_grp[g1].x) : 0u;
+        uint32_t tot = 0;
+        const uint32_t before = block_excl_scan(p0 + p1, s_tmp, &tot);
+        if (g0 < G) s_grp[g0].z = before;
+        if (g1 < G) s_grp[g1].z = before + p0;
+    }
+    __syncthreads();
+
+    // ---- phase 2: sweep the chunk space, groups wid, wid+4, ... ; U per round
+    for (uint32_t gr = wid; gr < G; gr += 4u * U) {
+        uint4 x[U];
+        uint32_t pos[U], mt[U], hlo[U], hhi[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = gr + 4u * u;
+            x[u] = make_uint4(0u, 0u, 0u, 0u);
+            pos[u] = 0;
+            mt[u] = 0;
+            hlo[u] = 0;
+            hhi[u] = 0;
+            if (g < G) {  // uniform
+                const uint4 gg = s_grp[g];
+                hlo[u] = uniform(gg.x);
+                hhi[u] = uniform(gg.y);
+                const uint32_t hb = uniform(gg.z);
+                const uint32_t j = g * 64u + lane;
+                const uint32_t excl = __builtin_amdgcn_mbcnt_hi(hhi[u], __builtin_amdgcn_mbcnt_lo(hlo[u], 0u));
+                const uint32_t own = (uint32_t)((((uint64_t)hhi[u] << 32) | hlo[u]) >> lane) & 1u;
+                if (j < C) {
+                    const uint32_t r = hb + excl + own - 1u;
+                    const uint4 rec = s_rec[r];
+                    const uint32_t k = j - rec.z;
+                    const uint64_t a = (((uint64_t)rec.y << 32) | rec.x) + 16ull * k;
+                    x[u] = load_nt(reinterpret_cast<const uint8_t*>(a));
+                    pos[u] = k;
+                    mt[u] = rec.w;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = gr + 4u * u;
+            if (g >= G) break;  // uniform
+            const uint32_t j = g * 64u + lane;
+            const bool valid = j < C;
+            uint4 v = x[u];
+            const uint32_t m = mt[u], k = pos[u];
+            const uint32_t lo = m & 15u, lastv = (m >> 4) & 31u, nchm1 = (m >> 10) & 127u;
+            const bool edge = valid && ((k == 0u && lo != 0u) || (k == nchm1 && lastv != 16u));
+            if (__builtin_amdgcn_ballot_w64(edge)) {
+                const int b0 = (k == 0u) ? (int)lo : 0;
+                const int b1 = (k == nchm1) ? (int)lastv : 16;
+                v.x &= byte_range_mask(b0, b1, 0);
+                v.y &= byte_range_mask(b0, b1, 1);
+                v.z &= byte_range_mask(b0, b1, 2);
+                v.w &= byte_range_mask(b0, b1, 3);
+            }
+            const bool odd = valid && (m & (1u << 9));
+            if (__builtin_amdgcn_ballot_w64(odd)) {
+                const uint32_t sel = odd ? 0x02030001u : 0x03020100u;
+                v.x = __builtin_amdgcn_perm(v.x, v.x, sel);
+                v.y = __builtin_amdgcn_perm(v.y, v.y, sel);
+                v.z = __builtin_amdgcn_perm(v.z, v.z, sel);
+                v.w = __builtin_amdgcn_perm(v.w, v.w, sel);
+            }
+            uint32_t val = 0;
+            val = dot2_acc(v.x, val);
+            val = dot2_acc(v.y, val);
+            val = dot2_acc(v.z, val);
+            val = dot2_acc(v.w, val);
+            if (!valid) val = 0;
+            const uint32_t P = wave_incl_scan(val);
+            // segment of this lane: from the last head at or below it (or lane 0)
+            const uint64_t H = (((uint64_t)hhi[u] << 32) | hlo[u]) | 1ull;
+            const uint64_t below = (lane == 63u) ? ~0ull : ((2ull << lane) - 1ull);
+            const uint64_t hm = H & below;
+            const uint32_t h = 63u - (uint32_t)__clzll(hm);
+            const uint32_t Ph = (uint32_t)__shfl((int)P, (int)(h == 0u ? 0u : h - 1u), 64);
+            const uint32_t seg = P - (h == 0u ? 0u : Ph);
+            const bool next_head = (lane < 63u) && ((H >> (lane + 1u)) & 1ull);
+            const bool tail = valid && (lane == 63u || j + 1u == C || next_head);
+            if (tail) atomicAdd(&s_acc[m >> 18], seg);
+        }
+    }
+
+    // ---- phase 3: packets longer than FCAP chunks, one wave each
+    for (uint32_t q = wid; q < nbig; q += 4u) {
+        const uint32_t tq = s_big[q];
+        const lvlip_csum_desc d = descs[tile0 + tq];
+        const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
+        const int lo = (int)(abs & 15ull);
+        const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
+        const uint32_t nchq = (uint32_t)((span + 15u) >> 4);
+        const uint32_t lastv = (uint32_t)(span - 16ull * (nchq - 1u));
+        const uint4* src = reinterpret_cast<const uint4*>(abs & ~15ull);
+        uint32_t w = (abs & 1ull) ? wave_packet_sum<4, true>(src, nchq, lo, lastv, lane)
+                                  : wave_packet_sum<4, false>(src, nchq, lo, lastv, lane);
+        w = wave_sum_dpp(w);
+        if (lane == 0) s_acc[tq] = w;
+    }
+    __syncthreads();
+
+    // ---- phase 4: fold and store (coalesced 2-B stores)
+    if (i_me < n) out[i_me] = finish(start_sum, s_acc[t]);
+}
 }  // namespace lvlip
 
 // ======================================================== host side (C ABI) ==
@@ -760,6 +989,20 @@ int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint
             break;
         }
         case LVLIP_KERNEL_FLAT: {
+            const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
+            if (unroll <= 0) unroll = 4;
+            switch (unroll) {
+                case 2: hipLaunchKernelGGL(lvlip::k_flat2<2>, dim3(grid), dim3(lvlip::FT), 0, s,
+                                           (const uint8_t*)base, descs, n, out); break;
+                case 4: hipLaunchKernelGGL(lvlip::k_flat2<4>, dim3(grid), dim3(lvlip::FT), 0, s,
+                                           (const uint8_t*)base, descs, n, out); break;
+                case 8: hipLaunchKernelGGL(lvlip::k_flat2<8>, dim3(grid), dim3(lvlip::FT), 0, s,
+                                           (const uint8_t*)base, descs, n, out); break;
+                default: return LVLIP_EINVAL;
+            }
+            break;
+        }
+        case 5: {  // first-generation flat kernel, kept for A/B measurement
             const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FLAT_T - 1) / lvlip::FLAT_T);
             hipLaunchKernelGGL(lvlip::k_flat, dim3(grid), dim3(lvlip::FLAT_T), 0, s,
                                (const uint8_t*)base, descs, n, out);

@@ -36,6 +36,9 @@ VARIANTS = [
     (lvlip.KERNEL_WAVE_LDS, 2, 0),
     (lvlip.KERNEL_WAVE_LDS, 4, 8),
     (lvlip.KERNEL_FLAT, 0, 0),
+    (lvlip.KERNEL_FLAT, 2, 0),
+    (lvlip.KERNEL_FLAT, 8, 0),
+    (5, 0, 0),                     # first-generation flat kernel (A/B)
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
@@ -199,7 +202,8 @@ def test_full_size_bit_exact(name):
     # size-independent property: every kernel variant agrees, and reruns are identical
     for variant in [(lvlip.KERNEL_WAVE, 4, 0), (lvlip.KERNEL_WAVE, 3, 4),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
-                    (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_AUTO, 0, 0)]:
+                    (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
+                    (lvlip.KERNEL_AUTO, 0, 0)]:
         assert np.array_equal(run(base, descs, variant, out), want), variant
     # adversarial packets really are there and fold as the reference does
     ones = b.paint == 2
