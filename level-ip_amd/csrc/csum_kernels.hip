@@ -322,13 +322,39 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
     fetch_window(descs, p_lo + 64u, n, lane, s_win[wid][1]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    // issue cursor: packet ip, byte offset io of the next piece in it
-    uint32_t ip = p_lo, io = 0;
-    PacketMeta cur = packet_meta(base, window_desc(s_win[wid][0], 0));
+    // Packet metadata for the issue cursor's window, one packet per lane (VALU,
+    // 64 packets at a time); the issue side pulls its packet's fields with
+    // v_readlane.  (Computing them per packet on the scalar unit made the
+    // kernel SALU-bound: r01 profile.)
+    uint32_t m_x, m_y, m_z, m_t, m_s;  // srd.x, srd.y, srd.z, tinfo, start of packet (window + lane)
+    auto load_window_meta = [&](uint32_t w) {
+        const uint4 d = s_win[wid][w & 1u][lane];
+        const PacketMeta pm = packet_meta(base, u32x4{d.x, d.y, d.z, d.w});
+        m_x = pm.srd.x;
+        m_y = pm.srd.y;
+        m_z = pm.srd.z;
+        m_t = pm.tinfo;
+        m_s = pm.start;
+    };
+    load_window_meta(0);
 
-    // consume side
-    uint32_t gc = p_lo;  // results of packets [gc, gc+64) gather in `res`
-    uint32_t res = 0;
+    // issue cursor: packet ip (k = ip - p_lo), byte offset io of the next piece in it
+    uint32_t ip = p_lo, io = 0;
+    u32x4 srd;
+    uint32_t tinfo, start;
+    auto pull = [&](uint32_t k) {  // k = packet index within its window
+        srd.x = (uint32_t)__builtin_amdgcn_readlane((int)m_x, (int)k);
+        srd.y = (uint32_t)__builtin_amdgcn_readlane((int)m_y, (int)k);
+        srd.z = (uint32_t)__builtin_amdgcn_readlane((int)m_z, (int)k);
+        srd.w = SRD_WORD3;
+        tinfo = (uint32_t)__builtin_amdgcn_readlane((int)m_t, (int)k);
+        start = (uint32_t)__builtin_amdgcn_readlane((int)m_s, (int)k);
+    };
+    pull(0);
+
+    // consume side: raw sums W and seeds of packets [gc, gc+64) gather in lanes
+    uint32_t gc = p_lo;
+    uint32_t res_w = 0, res_s = 0;
     uint32_t acc = 0;
 
     u32x4 va[R], vb[R];
@@ -338,18 +364,17 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
 
     auto issue = [&](int r) {
         const bool live = ip < p_hi;  // uniform
-        u32x4 srd = cur.srd;
-        if (!live) srd.z = 0;  // past the range: every dword out of range -> zeros
+        u32x4 sr = srd;
+        if (!live) sr.z = 0;  // past the range: every dword out of range -> zeros
         const uint32_t off = lane16 + io;
-        va[r] = buffer_load_nt_asm(off, srd);
-        vb[r] = buffer_load_nt_asm(off + 1024u, srd);
-        // cur.srd.z = round_up(len, 4): the piece is the packet's last when it
-        // reaches that (or the packet is empty)
-        const bool last = io + PIECE >= cur.srd.z;
-        const uint32_t lastdw = (cur.srd.z - 4u) - io;  // last dword, piece-relative
+        va[r] = buffer_load_nt_asm(off, sr);
+        vb[r] = buffer_load_nt_asm(off + 1024u, sr);
+        // srd.z = round_up(len, 4): the piece is the packet's last when it reaches
+        // that (or the packet is empty)
+        const bool last = io + PIECE >= srd.z;
         s_pkt[r] = live ? ip : END;
-        s_start[r] = cur.start;
-        s_meta[r] = (uint32_t)last | ((cur.tinfo & 3u) << 1) | (lastdw << 3);
+        s_start[r] = start;
+        s_meta[r] = (uint32_t)last | ((tinfo & 3u) << 1) | (((srd.z - 4u) - io) << 3);
         if (live) {
             if (!last) {
                 io += PIECE;
@@ -358,9 +383,11 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
                 io = 0;
                 if (ip < p_hi) {
                     const uint32_t k = ip - p_lo;
-                    if ((k & 63u) == 0u && k >= 64u)  // entered window k/64: refill the other
+                    if ((k & 63u) == 0u) {  // entered window k/64
+                        load_window_meta(k >> 6);
                         fetch_window(descs, ip + 64u, n, lane, s_win[wid][((k >> 6) + 1u) & 1u]);
-                    cur = packet_meta(base, window_desc(s_win[wid][(k >> 6) & 1u], k & 63u));
+                    }
+                    pull(k & 63u);
                 }
             }
         }
@@ -400,9 +427,16 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
             const uint32_t w = wave_sum_dpp(acc);
             acc = 0;
             const uint32_t k = s_pkt[r] - gc;
-            if (lane == k) res = finish(s_start[r], w);
+            if (lane == k) {
+                res_w = w;
+                res_s = s_start[r];
+            }
             if (k == 63u || s_pkt[r] + 1u == p_hi) {
-                if (lane <= k) out[gc + lane] = (uint16_t)res;
+                // fold 64 results at once (src/utils.c:46-54, per lane)
+                uint32_t tt = res_s + res_w;
+                tt = (tt & 0xffffu) + (tt >> 16);
+                tt = (tt & 0xffffu) + (tt >> 16);
+                if (lane <= k) out[gc + lane] = (uint16_t)~tt;
                 gc += 64u;
             }
         }
