@@ -109,6 +109,21 @@ __device__ __forceinline__ uint4 load_nt(const uint8_t* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Nontemporal 16-B load from a 64-bit global address held as an integer (the
+// cast to address space 1 keeps it a global_load; a generic pointer would make
+// it a flat_load, which counts on lgkmcnt too and serialises the waits).
+__device__ __forceinline__ uint4 load_nt_global(uint64_t a) {
+    typedef __attribute__((address_space(1))) const u32x4 gvec;
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<gvec*>(a));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint4 load_global(uint64_t a) {
+    typedef __attribute__((address_space(1))) const u32x4 gvec;
+    const u32x4 v = *reinterpret_cast<gvec*>(a);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // utils.c:46-54.  Two unconditional folds equal the reference's while loop:
 // after the first T <= 0x1fffe, after the second T <= 0xffff, and a fold of a
 // value <= 0xffff is the identity.
@@ -662,9 +677,11 @@ __global__ __launch_bounds__(FLAT_T) void k_flat(const uint8_t* __restrict__ bas
 // of 64 chunks per wave-load, U groups in flight per wave:
 //   rank   = heads before the group + v_mbcnt(heads below this lane) + own bit - 1
 //            (no search: the packet of every lane in two mbcnt instructions),
-//   bytes  = 16-B aligned loads from the packet's own address (coalesced across
-//            packet boundaries), first/last chunk bytes masked, odd-address
-//            packets byte-swapped within u16 halves (v_perm),
+//   bytes  = whole 16-B aligned chunks from the packet's own address
+//            (coalesced across packet boundaries), odd-address packets
+//            byte-swapped within u16 halves (v_perm); no per-lane masking:
+//            phase 1 seeds each packet's accumulator with minus the sum of the
+//            bytes of its first/last chunk that lie outside it (mod 2^32),
 //   reduce = inclusive DPP prefix sum over the wave; each segment's tail lane
 //            takes P(tail) - P(head-1) and adds it to the packet's u32
 //            accumulator in LDS (mod-2^32 adds: exact in any order).
@@ -734,7 +751,7 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
     const uint32_t i_me = tile0 + t;
 
     // ---- phase 1: descriptors -> chunk counts, ranks, records, head bitmap
-    uint32_t start_sum = 0, nch = 0, meta = 0;
+    uint32_t start_sum = 0, nch = 0, meta = 0, corr = 0;
     uint64_t a0 = 0;
     bool big = false;
     if (i_me < n) {
@@ -747,13 +764,35 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
             const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
             const uint64_t c64 = (span + 15u) >> 4;
             const uint32_t lastv = (uint32_t)(span - 16ull * (c64 - 1u));
+            const bool odd = abs & 1ull;
             big = c64 > FCAP;
             nch = big ? 0u : (uint32_t)c64;
-            meta = lo | (lastv << 4) | ((uint32_t)(abs & 1ull) << 9) |
-                   (((uint32_t)(c64 - 1u) & 127u) << 10) | (t << 18);
+            meta = ((uint32_t)odd << 9) | (t << 18);
+            if (!big && (lo != 0u || lastv != 16u)) {
+                // The sweep sums whole 16-B chunks; subtract here, once per packet,
+                // the bytes of the first and last chunk that lie outside it (same
+                // parity convention, mod 2^32 — exact).
+                const uint4 f = load_global(a0);
+                const int fb1 = (c64 == 1u) ? (int)lastv : 16;
+                uint4 out_f = f;  // bytes of the first chunk outside [lo, fb1)
+                out_f.x &= ~byte_range_mask((int)lo, fb1, 0);
+                out_f.y &= ~byte_range_mask((int)lo, fb1, 1);
+                out_f.z &= ~byte_range_mask((int)lo, fb1, 2);
+                out_f.w &= ~byte_range_mask((int)lo, fb1, 3);
+                uint32_t c = odd ? chunk_words<true>(out_f) : chunk_words<false>(out_f);
+                if (c64 > 1u && lastv != 16u) {
+                    uint4 out_l = load_global(a0 + 16ull * (c64 - 1u));
+                    out_l.x &= ~byte_range_mask(0, (int)lastv, 0);
+                    out_l.y &= ~byte_range_mask(0, (int)lastv, 1);
+                    out_l.z &= ~byte_range_mask(0, (int)lastv, 2);
+                    out_l.w &= ~byte_range_mask(0, (int)lastv, 3);
+                    c += odd ? chunk_words<true>(out_l) : chunk_words<false>(out_l);
+                }
+                corr = c;
+            }
         }
     }
-    s_acc[t] = 0;
+    s_acc[t] = 0u - corr;
     for (uint32_t g = t; g < FGROUPS; g += FT) s_grp[g] = make_uint4(0u, 0u, 0u, 0u);
     uint32_t nbig = 0;
     const uint32_t big_pos = block_excl_scan(big ? 1u : 0u, s_tmp, &nbig);
@@ -782,80 +821,75 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
     }
     __syncthreads();
 
-    // ---- phase 2: sweep the chunk space, groups wid, wid+4, ... ; U per round
-    for (uint32_t gr = wid; gr < G; gr += 4u * U) {
-        uint4 x[U];
-        uint32_t pos[U], mt[U], hlo[U], hhi[U];
+    // ---- phase 2: sweep the chunk space, groups wid, wid+4, ... ; U per round.
+    // Every round issues exactly U loads, unconditionally (lanes past the chunk
+    // space read a valid chunk of the tile's first packet and are zeroed), after
+    // all U group headers and all U records are in registers: hipcc then retires
+    // them with counted vmcnt waits instead of draining.
+    if (C > 0) {
+        for (uint32_t gr = wid; gr < G; gr += 4u * U) {
+            uint4 x[U];
+            uint32_t mt[U], hlo[U], hhi[U], hb[U], r[U];
+            bool gv[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t g = gr + 4u * u;
-            x[u] = make_uint4(0u, 0u, 0u, 0u);
-            pos[u] = 0;
-            mt[u] = 0;
-            hlo[u] = 0;
-            hhi[u] = 0;
-            if (g < G) {  // uniform
-                const uint4 gg = s_grp[g];
+            for (int u = 0; u < U; ++u) {
+                const uint32_t g = gr + 4u * u;
+                gv[u] = g < G;
+                const uint4 gg = s_grp[gv[u] ? g : G - 1u];
                 hlo[u] = uniform(gg.x);
                 hhi[u] = uniform(gg.y);
-                const uint32_t hb = uniform(gg.z);
-                const uint32_t j = g * 64u + lane;
+                hb[u] = uniform(gg.z);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t j = (gr + 4u * u) * 64u + lane;
                 const uint32_t excl = __builtin_amdgcn_mbcnt_hi(hhi[u], __builtin_amdgcn_mbcnt_lo(hlo[u], 0u));
                 const uint32_t own = (uint32_t)((((uint64_t)hhi[u] << 32) | hlo[u]) >> lane) & 1u;
-                if (j < C) {
-                    const uint32_t r = hb + excl + own - 1u;
-                    const uint4 rec = s_rec[r];
-                    const uint32_t k = j - rec.z;
-                    const uint64_t a = (((uint64_t)rec.y << 32) | rec.x) + 16ull * k;
-                    x[u] = load_nt(reinterpret_cast<const uint8_t*>(a));
-                    pos[u] = k;
-                    mt[u] = rec.w;
-                }
+                r[u] = (gv[u] && j < C) ? hb[u] + excl + own - 1u : 0u;
             }
-        }
+            uint4 rec[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t g = gr + 4u * u;
-            if (g >= G) break;  // uniform
-            const uint32_t j = g * 64u + lane;
-            const bool valid = j < C;
-            uint4 v = x[u];
-            const uint32_t m = mt[u], k = pos[u];
-            const uint32_t lo = m & 15u, lastv = (m >> 4) & 31u, nchm1 = (m >> 10) & 127u;
-            const bool edge = valid && ((k == 0u && lo != 0u) || (k == nchm1 && lastv != 16u));
-            if (__builtin_amdgcn_ballot_w64(edge)) {
-                const int b0 = (k == 0u) ? (int)lo : 0;
-                const int b1 = (k == nchm1) ? (int)lastv : 16;
-                v.x &= byte_range_mask(b0, b1, 0);
-                v.y &= byte_range_mask(b0, b1, 1);
-                v.z &= byte_range_mask(b0, b1, 2);
-                v.w &= byte_range_mask(b0, b1, 3);
+            for (int u = 0; u < U; ++u) rec[u] = s_rec[r[u]];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t j = (gr + 4u * u) * 64u + lane;
+                const bool valid = gv[u] && j < C;
+                const uint32_t k = valid ? j - rec[u].z : 0u;
+                x[u] = load_nt_global((((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * k);
+                mt[u] = rec[u].w;
             }
-            const bool odd = valid && (m & (1u << 9));
-            if (__builtin_amdgcn_ballot_w64(odd)) {
-                const uint32_t sel = odd ? 0x02030001u : 0x03020100u;
-                v.x = __builtin_amdgcn_perm(v.x, v.x, sel);
-                v.y = __builtin_amdgcn_perm(v.y, v.y, sel);
-                v.z = __builtin_amdgcn_perm(v.z, v.z, sel);
-                v.w = __builtin_amdgcn_perm(v.w, v.w, sel);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!gv[u]) break;  // uniform
+                const uint32_t j = (gr + 4u * u) * 64u + lane;
+                const bool valid = j < C;
+                uint4 v = x[u];
+                const uint32_t m = mt[u];
+                const bool odd = valid && (m & (1u << 9));
+                if (__builtin_amdgcn_ballot_w64(odd)) {
+                    const uint32_t sel = odd ? 0x02030001u : 0x03020100u;
+                    v.x = __builtin_amdgcn_perm(v.x, v.x, sel);
+                    v.y = __builtin_amdgcn_perm(v.y, v.y, sel);
+                    v.z = __builtin_amdgcn_perm(v.z, v.z, sel);
+                    v.w = __builtin_amdgcn_perm(v.w, v.w, sel);
+                }
+                uint32_t val = 0;
+                val = dot2_acc(v.x, val);
+                val = dot2_acc(v.y, val);
+                val = dot2_acc(v.z, val);
+                val = dot2_acc(v.w, val);
+                if (!valid) val = 0;
+                const uint32_t P = wave_incl_scan(val);
+                // segment of this lane: from the last head at or below it (or lane 0)
+                const uint64_t H = (((uint64_t)hhi[u] << 32) | hlo[u]) | 1ull;
+                const uint64_t below = (lane == 63u) ? ~0ull : ((2ull << lane) - 1ull);
+                const uint32_t h = 63u - (uint32_t)__clzll(H & below);
+                const uint32_t Ph = (uint32_t)__shfl((int)P, (int)(h == 0u ? 0u : h - 1u), 64);
+                const uint32_t seg = P - (h == 0u ? 0u : Ph);
+                const bool next_head = (lane < 63u) && ((H >> (lane + 1u)) & 1ull);
+                const bool tail = valid && (lane == 63u || j + 1u == C || next_head);
+                if (tail) atomicAdd(&s_acc[m >> 18], seg);
             }
-            uint32_t val = 0;
-            val = dot2_acc(v.x, val);
-            val = dot2_acc(v.y, val);
-            val = dot2_acc(v.z, val);
-            val = dot2_acc(v.w, val);
-            if (!valid) val = 0;
-            const uint32_t P = wave_incl_scan(val);
-            // segment of this lane: from the last head at or below it (or lane 0)
-            const uint64_t H = (((uint64_t)hhi[u] << 32) | hlo[u]) | 1ull;
-            const uint64_t below = (lane == 63u) ? ~0ull : ((2ull << lane) - 1ull);
-            const uint64_t hm = H & below;
-            const uint32_t h = 63u - (uint32_t)__clzll(hm);
-            const uint32_t Ph = (uint32_t)__shfl((int)P, (int)(h == 0u ? 0u : h - 1u), 64);
-            const uint32_t seg = P - (h == 0u ? 0u : Ph);
-            const bool next_head = (lane < 63u) && ((H >> (lane + 1u)) & 1ull);
-            const bool tail = valid && (lane == 63u || j + 1u == C || next_head);
-            if (tail) atomicAdd(&s_acc[m >> 18], seg);
         }
     }
 
