@@ -87,7 +87,7 @@ def traffic_from_profiles(workload: str, kernel_label: str):
     return best
 
 
-def cpu_baseline(b, threads: int, kernel: int, unroll: int, wpc: int, dev,
+def cpu_baseline(b, threads: int, kernel: int, unroll: int, wpc: int, dev, len_hint: int = 0,
                  budget_s: float = 1.0):
     """Reference checksum() over a bounded sample of the same workload on the host.
 
@@ -107,7 +107,7 @@ def cpu_baseline(b, threads: int, kernel: int, unroll: int, wpc: int, dev,
     ref_out = pyoracle.batch(host, sb.descs, threads=threads, opt=0, use_reference=use_ref)
     sbase, sdescs, sout = workloads.to_device(sb, dev)
     lvlip.batch_dev(sbase.data_ptr(), sdescs.data_ptr(), sb.n, sout.data_ptr(),
-                    torch.cuda.current_stream(dev).cuda_stream, kernel, unroll, wpc)
+                    torch.cuda.current_stream(dev).cuda_stream, kernel, unroll, wpc, len_hint)
     torch.cuda.synchronize(dev)
     verified = bool(np.array_equal(sout.cpu().numpy().view(np.uint16), ref_out))
     if not verified:
@@ -177,9 +177,12 @@ def main():
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
 
+    # the batch's average packet length, as a caller that built it knows it
+    len_hint = b.algo_bytes // max(1, b.n)
+
     def step():
         lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(), stream.cuda_stream,
-                        kernel, args.unroll, args.waves_per_cu)
+                        kernel, args.unroll, args.waves_per_cu, len_hint)
 
     for _ in range(args.warmup):
         step()
@@ -212,6 +215,9 @@ def main():
     value = total_bytes * args.steps / wall_max / 1e9
     achieved = b.algo_bytes / (kern_ms / 1e3) / 1e9  # rank 0's kernel, algorithmic bytes
     kernel_label = f"{args.kernel}-u{args.unroll}-w{args.waves_per_cu}"
+    chosen = ({lvlip.KERNEL_WAVE: "wave", lvlip.KERNEL_FLAT: "flat"}[
+        lvlip.KERNEL_WAVE if len_hint >= 512 else lvlip.KERNEL_FLAT]
+        if kernel == lvlip.KERNEL_AUTO else args.kernel)
 
     diag = {}
     if rank == 0 and args.sweep:
@@ -224,7 +230,8 @@ def main():
     cpu, verified = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, verified = cpu_baseline(b, threads=min(16, os.cpu_count() or 1), kernel=kernel,
-                                     unroll=args.unroll, wpc=args.waves_per_cu, dev=dev)
+                                     unroll=args.unroll, wpc=args.waves_per_cu, dev=dev,
+                                     len_hint=len_hint)
 
     if rank == 0:
         rec = {
@@ -236,7 +243,8 @@ def main():
                     "device-resident",
             "config": {"workload": f"{args.workload}: {WORKLOAD_TEXT[args.workload]}",
                        "descriptors_per_gpu": b.n, "bytes_per_gpu": b.algo_bytes,
-                       "kernel": kernel_label, "parallelism": f"shard{world} (no collective)"},
+                       "kernel": kernel_label, "kernel_selected": chosen,
+                       "len_hint": len_hint, "parallelism": f"shard{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic_from_profiles(args.workload, kernel_label),

@@ -99,8 +99,10 @@ typedef struct lvlip_csum_desc {
 int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
                          uint32_t n, uint16_t *out, void *stream);
 
-/* Kernel selection for lvlip_csum_batch_dev_ex (benchmarks, A/B tests). */
-#define LVLIP_KERNEL_AUTO        0  /* the default (kernel choice)  */
+/* Kernel selection for lvlip_csum_batch_dev_ex.  AUTO picks by len_hint:
+ * >= 512 B -> WAVE (8 waves/CU from 4 KiB up, else 16), otherwise or unknown ->
+ * FLAT (measured: DESIGN.md §5). */
+#define LVLIP_KERNEL_AUTO        0  /* the default                                 */
 #define LVLIP_KERNEL_WAVE        1  /* one wavefront per packet, persistent stream */
 #define LVLIP_KERNEL_WAVE_LDS    2  /* one wave per packet, LDS-DMA staging (A/B)  */
 #define LVLIP_KERNEL_FLAT        3  /* chunk-balanced tile sweep (ragged batches)  */
@@ -111,7 +113,8 @@ typedef struct lvlip_launch_cfg {
     int32_t  unroll;        /* 16-B loads in flight per lane (0 = default)  */
     int32_t  waves_per_cu;  /* WAVE: resident waves per CU (0 = 8); others:
                                grid cap (0 = one wave per packet)           */
-    int32_t  reserved;      /* must be 0                                    */
+    int32_t  len_hint;      /* average packet length in bytes if the caller
+                               knows it (AUTO uses it), 0 = unknown         */
 } lvlip_launch_cfg;
 
 int lvlip_csum_batch_dev_ex(const void *base, const lvlip_csum_desc *descs,

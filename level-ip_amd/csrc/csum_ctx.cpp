@@ -101,9 +101,8 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
                             hipMemcpyHostToDevice, s.stream)) != hipSuccess)
         return fail(c, e, "H2D descriptors");
     lvlip_launch_cfg cfg{};
-    // Gathered pieces are mixed-size skbs by nature; the flat tile sweep keeps
-    // every lane busy on short headers (kernel choice).
-    cfg.kernel = (bytes / count >= 1024) ? LVLIP_KERNEL_WAVE : LVLIP_KERNEL_FLAT;
+    cfg.kernel = LVLIP_KERNEL_AUTO;  // the piece's average length picks the kernel
+    cfg.len_hint = (int32_t)(bytes / count > 0x7fffffffull ? 0x7fffffff : bytes / count);
     int rc = lvlip_csum_batch_dev_ex(s.d_bytes, s.d_desc, count, s.d_out, s.stream, &cfg);
     if (rc != LVLIP_OK) return rc;
     if ((e = hipMemcpyAsync(s.h_out, s.d_out, (size_t)count * sizeof(uint16_t),

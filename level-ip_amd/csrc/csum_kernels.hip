@@ -1016,12 +1016,23 @@ int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint
     if (!base || !descs || !out || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
     if (((uintptr_t)base & 15u) != 0) return LVLIP_EINVAL;
     hipStream_t s = (hipStream_t)stream;
-    const int kernel = cfg ? cfg->kernel : LVLIP_KERNEL_AUTO;
+    int kernel = cfg ? cfg->kernel : LVLIP_KERNEL_AUTO;
     int unroll = cfg ? cfg->unroll : 0;
-    const int wpc = cfg ? cfg->waves_per_cu : 0;
+    int wpc = cfg ? cfg->waves_per_cu : 0;
+    if (kernel == LVLIP_KERNEL_AUTO) {
+        // Measured on MI355X: the stream kernel leads on uniform
+        // MTU/jumbo segments, the flat sweep on mixed header/payload batches and
+        // stays within ~10 % elsewhere, so it is the choice when sizes are unknown.
+        const int hint = cfg ? cfg->len_hint : 0;
+        if (hint >= 512) {
+            kernel = LVLIP_KERNEL_WAVE;
+            if (wpc <= 0) wpc = hint >= 4096 ? 8 : 16;
+        } else {
+            kernel = LVLIP_KERNEL_FLAT;
+        }
+    }
 
     switch (kernel) {
-        case LVLIP_KERNEL_AUTO:
         case LVLIP_KERNEL_WAVE: {
             // unroll = 2-KiB pieces in flight per wave (2 = up to 4 KiB)
             if (unroll <= 0) unroll = 2;

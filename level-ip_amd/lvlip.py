@@ -57,7 +57,7 @@ class LvlipError(RuntimeError):
 
 class LaunchCfg(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_int32), ("unroll", ctypes.c_int32),
-                ("waves_per_cu", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("waves_per_cu", ctypes.c_int32), ("len_hint", ctypes.c_int32)]
 
 
 class Iov(ctypes.Structure):
@@ -184,15 +184,16 @@ def ip_send_check(hdr: bytearray) -> None:
 # ---------------------------------------------------------- device batches --
 
 def batch_dev(base_ptr: int, desc_ptr: int, n: int, out_ptr: int, stream: int = 0,
-              kernel: int = KERNEL_AUTO, unroll: int = 0, waves_per_cu: int = 0) -> None:
+              kernel: int = KERNEL_AUTO, unroll: int = 0, waves_per_cu: int = 0,
+              len_hint: int = 0) -> None:
     """lvlip_csum_batch_dev_ex on raw device pointers (async on `stream`)."""
-    cfg = LaunchCfg(kernel, unroll, waves_per_cu, 0)
+    cfg = LaunchCfg(kernel, unroll, waves_per_cu, min(max(int(len_hint), 0), 0x7FFFFFFF))
     _check(_lib.lvlip_csum_batch_dev_ex(base_ptr, desc_ptr, n, out_ptr, stream or None,
                                         ctypes.byref(cfg)), "lvlip_csum_batch_dev_ex")
 
 
 def batch_torch(base, descs, out=None, kernel: int = KERNEL_AUTO, unroll: int = 0,
-                waves_per_cu: int = 0, stream=None):
+                waves_per_cu: int = 0, stream=None, len_hint: int = 0):
     """Checksums a device batch held in torch tensors on the current stream.
 
     base:  uint8 CUDA tensor (16-B aligned, padded to a 16-B multiple past the last packet)
@@ -209,7 +210,7 @@ def batch_torch(base, descs, out=None, kernel: int = KERNEL_AUTO, unroll: int = 
     if stream is None:
         stream = torch.cuda.current_stream(base.device)
     batch_dev(base.data_ptr(), descs.data_ptr(), n, out.data_ptr(), stream.cuda_stream,
-              kernel, unroll, waves_per_cu)
+              kernel, unroll, waves_per_cu, len_hint)
     return out
 
 

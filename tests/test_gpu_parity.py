@@ -187,6 +187,11 @@ def test_configs_small_all_kernels(name, n):
     for variant in VARIANTS:
         got = run(base, descs, variant, out)
         assert np.array_equal(got, want), variant
+    # AUTO with the caller's length hint (selects the stream kernel for MTU/jumbo)
+    hint = b.algo_bytes // b.n
+    lvlip.batch_torch(base, descs, out, len_hint=hint)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
 
 
 @pytest.mark.parametrize("name", ["tcp1500", "tcp9000", "mixed"])
@@ -194,7 +199,9 @@ def test_full_size_bit_exact(name):
     """BASELINE configs #2-#4 at full size: all N outputs vs the oracle on the same bytes."""
     b = workloads.make(name)
     base, descs, out = workloads.to_device(b)
-    got_auto = run(base, descs, (lvlip.KERNEL_AUTO, 0, 0), out)
+    lvlip.batch_torch(base, descs, out, len_hint=b.algo_bytes // b.n)
+    torch.cuda.synchronize()
+    got_auto = out.cpu().numpy().view(np.uint16)
     host = base.cpu().numpy()
     want = pyoracle.batch(host, b.descs, threads=THREADS)
     bad = np.nonzero(got_auto != want)[0]
