@@ -1,0 +1,103 @@
+/*
+ * lvlip_skb.h — batch-and-dispatch over level-ip frames.
+ *
+ * level-ip handles one frame at a time: netdev_rx_loop reads one frame per
+ * read(2) (src/netdev.c:86-101) and every checksum is a synchronous per-packet
+ * call.  These entry points take N frames at once and run all their checksums
+ * as ONE GPU batch through a context (include/lvlip_csum.h, Group 3).
+ *
+ * A frame is what an sk_buff holds (include/skbuff.h:9-23): `head` points at the
+ * Ethernet header, the IPv4 header is at head + 14 (ip_hdr(), include/ip.h:47-50)
+ * and the TCP/ICMP header right after it (tcp_hdr(), include/tcp.h:224-227).
+ *
+ * Each call is plan -> one batch -> apply.  The plan and apply steps are
+ * exported too: they are plain host logic (no GPU) and are what the CPU tests
+ * exercise.
+ */
+#ifndef LVLIP_SKB_H
+#define LVLIP_SKB_H
+
+#include <stdint.h>
+
+#include "lvlip_csum.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+#pragma GCC visibility push(default)
+
+typedef struct lvlip_frame {
+    uint8_t *head;  /* Ethernet header (skb->head) */
+    uint32_t len;   /* bytes valid from head */
+} lvlip_frame;
+
+/* ---- f1: RX ------------------------------------------------------------ */
+
+/* Verdicts, in the order ip_rcv (src/ip_input.c:17-43) takes its decisions. */
+#define LVLIP_RX_OK          1  /* ip_rcv hands the packet to icmpv4_incoming/tcp_in */
+#define LVLIP_RX_NOT_IP      2  /* ethertype != 0x0800 (netdev_receive, src/netdev.c:67-80) */
+#define LVLIP_RX_SHORT       3  /* frame shorter than 14 + 20, 14 + ihl*4, or (with
+                                   VERIFY_L4) 14 + the IP total length; the
+                                   reference has no such check (it would read past
+                                   the frame) */
+#define LVLIP_RX_BAD_VERSION 4  /* src/ip_input.c:22-25                          */
+#define LVLIP_RX_BAD_IHL     5  /* src/ip_input.c:27-30                          */
+#define LVLIP_RX_TTL0        6  /* src/ip_input.c:32-36                          */
+#define LVLIP_RX_BAD_CSUM    7  /* checksum(ih, ihl*4, 0) != 0, src/ip_input.c:38-43 */
+#define LVLIP_RX_BAD_L4      8  /* only with LVLIP_RX_VERIFY_L4                  */
+#define LVLIP_RX_UNKNOWN_PROTO 9 /* not ICMP/TCP, src/ip_input.c:51-60         */
+
+/* Also verify TCP (pseudo header, RFC arithmetic: the seed's carries are folded
+ * back in) and ICMP checksums.  The reference never verifies them on RX
+ * (src/tcp.c:79-81 is commented out, src/icmpv4.c:11 is a TODO), so this is off
+ * by default. */
+#define LVLIP_RX_VERIFY_L4   0x1u
+
+/* Verdict per frame; frames are not modified.  Must run before ip_init_pkt's
+ * in-place byte swaps (src/ip_input.c:47).  Returns 0 or LVLIP_E*. */
+int lvlip_rx_verify(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n,
+                    uint32_t flags, uint8_t *verdict);
+
+/* Plan: verdict[] gets the header-field decisions, or 0 / 0x80|X = pending on
+ * the checksums (X is the verdict if the header checksum passes);
+ * iov[]/tag[] (capacity 2n) get the checksums to run, tag = frame << 1 | is_l4.
+ * Returns the number of iov entries. */
+uint32_t lvlip_rx_plan(const lvlip_frame *frames, uint32_t n, uint32_t flags,
+                       uint8_t *verdict, lvlip_csum_iov *iov, uint32_t *tag);
+/* Apply: BAD_CSUM if the header checksum fails, else BAD_L4 if an L4 one does,
+ * else the deferred verdict (OK for 0). */
+void lvlip_rx_apply(uint32_t n, uint8_t *verdict, uint32_t m, const uint32_t *tag,
+                    const uint16_t *csum);
+
+/* ---- f2: TX ------------------------------------------------------------ */
+
+/* Frames fully built by tcp_transmit_skb / ip_output / icmpv4_reply except their
+ * checksums.  Fills, stored raw as the reference stores them, the values the
+ * reference computes with each field zeroed first (whatever the field holds):
+ *   TCP  : checksum(tcp, ip.len - ihl*4, pseudo(saddr, daddr, 6, len))
+ *          src/tcp_output.c:110,126 -> src/tcp.c:87-98 (u32 seed, carry lost);
+ *          saddr/daddr are the header's network-order words, as
+ *          tcp_transmit_skb passes htonl(sk->saddr), htonl(sk->daddr)
+ *   ICMP : checksum(icmp, ip.len - ihl*4, 0), src/icmpv4.c:46-47
+ *   IPv4 : checksum(ih, ihl*4, 0), src/ip_output.c:42,53 (ip_send_check)
+ * The IPv4 header checksum does not cover the L4 bytes, so all 2n checksums
+ * are one batch.  Returns 0 or LVLIP_E* (frames untouched on error). */
+int lvlip_tx_checksum(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n);
+
+/* Plan: fills iov[]/field[] (capacity 2n; field = where each result goes),
+ * frames unmodified (each seed is compensated for its field's current value).
+ * Returns the number of iov entries, or 0xFFFFFFFF if a frame is malformed. */
+uint32_t lvlip_tx_plan(lvlip_frame *frames, uint32_t n, lvlip_csum_iov *iov,
+                       uint8_t **field);
+void lvlip_tx_apply(uint32_t m, uint8_t *const *field, const uint16_t *csum);
+
+/* RFC 1071 pseudo-header seed with the carries folded back (for RX verify of
+ * checksums produced by RFC-correct peers). */
+uint32_t lvlip_pseudo_sum_rfc(uint32_t saddr, uint32_t daddr, uint8_t proto,
+                              uint16_t len);
+
+#pragma GCC visibility pop
+#ifdef __cplusplus
+}
+#endif
+#endif /* LVLIP_SKB_H */

@@ -1,0 +1,216 @@
+/*
+ * skb_batch.c — f1/f2 of SURVEY.md §8f: batch-and-dispatch over level-ip frames.
+ * See include/lvlip_skb.h for the contract; every decision cites the reference
+ * line it mirrors.  Host logic only; the checksums themselves run as one GPU
+ * batch through lvlip_csum_batch_host (csum_ctx.cpp).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "lvlip_skb.h"
+
+#define ETH_HDR_LEN 14u   /* include/ethernet.h: struct eth_hdr, 14 B packed */
+#define ETH_P_IP 0x0800u
+#define PROTO_ICMP 1u     /* include/ip.h: ICMPV4 */
+#define PROTO_TCP 6u      /* include/ip.h: IP_TCP */
+#define PENDING 0x80u     /* rx_plan: verdict decided once the header checksum is known */
+
+static inline uint16_t be16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+static inline uint32_t le32(const uint8_t *p)
+{
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return v;
+}
+static inline uint16_t bswap16(uint16_t x) { return (uint16_t)((x << 8) | (x >> 8)); }
+static inline uint32_t le16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+
+uint32_t lvlip_pseudo_sum_rfc(uint32_t saddr, uint32_t daddr, uint8_t proto, uint16_t len)
+{
+    /* the same words the reference adds (src/tcp.c:92-95), but as 16-bit halves so
+     * no carry is lost: sum < 6 * 0xffff, folded by the checksum's final fold */
+    return (saddr & 0xffffu) + (saddr >> 16) + (daddr & 0xffffu) + (daddr >> 16) +
+           bswap16((uint16_t)proto) + bswap16(len);
+}
+
+/* ----------------------------------------------------------------- f1: RX */
+
+uint32_t lvlip_rx_plan(const lvlip_frame *frames, uint32_t n, uint32_t flags,
+                       uint8_t *verdict, lvlip_csum_iov *iov, uint32_t *tag)
+{
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t *h = frames[i].head;
+        const uint32_t flen = frames[i].len;
+        verdict[i] = 0;
+        if (!h || flen < ETH_HDR_LEN + 20u) {
+            verdict[i] = LVLIP_RX_SHORT;
+            continue;
+        }
+        if (be16(h + 12) != ETH_P_IP) { /* netdev_receive dispatch, src/netdev.c:67-80 */
+            verdict[i] = LVLIP_RX_NOT_IP;
+            continue;
+        }
+        const uint8_t *ih = h + ETH_HDR_LEN;
+        const uint32_t version = ih[0] >> 4, ihl = ih[0] & 0x0fu; /* ihl:4 low nibble, include/ip.h:33-34 */
+        if (version != 4u) { /* src/ip_input.c:22 */
+            verdict[i] = LVLIP_RX_BAD_VERSION;
+            continue;
+        }
+        if (ihl < 5u) { /* src/ip_input.c:27 */
+            verdict[i] = LVLIP_RX_BAD_IHL;
+            continue;
+        }
+        if (ih[8] == 0u) { /* ttl, src/ip_input.c:32 */
+            verdict[i] = LVLIP_RX_TTL0;
+            continue;
+        }
+        if (flen < ETH_HDR_LEN + ihl * 4u) {
+            verdict[i] = LVLIP_RX_SHORT;
+            continue;
+        }
+        /* checksum(ih, ihl*4, 0) must be 0, src/ip_input.c:38-43 */
+        iov[m].ptr = ih;
+        iov[m].len = (int32_t)(ihl * 4u);
+        iov[m].start_sum = 0;
+        tag[m++] = i << 1;
+        /* decided after the checksum (ip_rcv checks it first): a pending
+         * verdict PENDING|X becomes X if the header checksum passes */
+        const uint32_t proto = ih[9];
+        if (proto != PROTO_TCP && proto != PROTO_ICMP) { /* src/ip_input.c:51-60 */
+            verdict[i] = PENDING | LVLIP_RX_UNKNOWN_PROTO;
+            continue;
+        }
+        if (flags & LVLIP_RX_VERIFY_L4) {
+            const uint32_t iplen = be16(ih + 2);
+            if (iplen < ihl * 4u || flen < ETH_HDR_LEN + iplen) {
+                verdict[i] = PENDING | LVLIP_RX_SHORT;
+                continue;
+            }
+            const uint32_t l4len = iplen - ihl * 4u;
+            iov[m].ptr = ih + ihl * 4u;
+            iov[m].len = (int32_t)l4len;
+            iov[m].start_sum = proto == PROTO_TCP
+                                   ? lvlip_pseudo_sum_rfc(le32(ih + 12), le32(ih + 16), PROTO_TCP,
+                                                          (uint16_t)l4len)
+                                   : 0u;
+            tag[m++] = (i << 1) | 1u;
+        }
+    }
+    return m;
+}
+
+static inline int pending(uint8_t v) { return v == 0 || (v & PENDING); }
+
+void lvlip_rx_apply(uint32_t n, uint8_t *verdict, uint32_t m, const uint32_t *tag,
+                    const uint16_t *csum)
+{
+    (void)n;
+    /* every pending frame has its header entry, so walking the entries reaches
+     * all of them: header checksum first, then L4, then the deferred verdict */
+    for (uint32_t k = 0; k < m; k++)
+        if (!(tag[k] & 1u) && csum[k] != 0 && pending(verdict[tag[k] >> 1]))
+            verdict[tag[k] >> 1] = LVLIP_RX_BAD_CSUM;
+    for (uint32_t k = 0; k < m; k++)
+        if ((tag[k] & 1u) && csum[k] != 0 && verdict[tag[k] >> 1] == 0)
+            verdict[tag[k] >> 1] = LVLIP_RX_BAD_L4;
+    for (uint32_t k = 0; k < m; k++) {
+        uint8_t *v = &verdict[tag[k] >> 1];
+        if (pending(*v)) *v = *v ? (uint8_t)(*v & ~PENDING) : (uint8_t)LVLIP_RX_OK;
+    }
+}
+
+int lvlip_rx_verify(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n, uint32_t flags,
+                    uint8_t *verdict)
+{
+    if (!ctx || (n && (!frames || !verdict))) return LVLIP_EINVAL;
+    if (n == 0) return LVLIP_OK;
+    lvlip_csum_iov *iov = (lvlip_csum_iov *)malloc(sizeof(lvlip_csum_iov) * 2u * (size_t)n);
+    uint32_t *tag = (uint32_t *)malloc(sizeof(uint32_t) * 2u * (size_t)n);
+    uint16_t *cs = (uint16_t *)malloc(sizeof(uint16_t) * 2u * (size_t)n);
+    int rc = LVLIP_ENOMEM;
+    if (iov && tag && cs) {
+        const uint32_t m = lvlip_rx_plan(frames, n, flags, verdict, iov, tag);
+        rc = m ? lvlip_csum_batch_host(ctx, iov, m, cs) : LVLIP_OK;
+        if (rc == LVLIP_OK) lvlip_rx_apply(n, verdict, m, tag, cs);
+    }
+    free(iov);
+    free(tag);
+    free(cs);
+    return rc;
+}
+
+/* ----------------------------------------------------------------- f2: TX */
+
+uint32_t lvlip_tx_plan(lvlip_frame *frames, uint32_t n, lvlip_csum_iov *iov, uint8_t **field)
+{
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t *h = frames[i].head;
+        if (!h || frames[i].len < ETH_HDR_LEN + 20u) return 0xFFFFFFFFu;
+        uint8_t *ih = h + ETH_HDR_LEN;
+        const uint32_t ihl = ih[0] & 0x0fu, iplen = be16(ih + 2), proto = ih[9];
+        if ((ih[0] >> 4) != 4u || ihl < 5u || iplen < ihl * 4u ||
+            frames[i].len < ETH_HDR_LEN + iplen)
+            return 0xFFFFFFFFu;
+        uint8_t *l4 = ih + ihl * 4u;
+        const uint32_t l4len = iplen - ihl * 4u;
+        /* The reference zeroes each checksum field before summing
+         * (src/tcp_output.c:110, src/icmpv4.c:46, src/ip_output.c:42).  Instead
+         * of writing the frame now, the field's current u16 (an even offset, so
+         * it is exactly one summed word) is subtracted from the seed: mod 2^32
+         * that is the same T, and a failed batch leaves the frame untouched. */
+        if (proto == PROTO_TCP && l4len >= 20u) {
+            iov[m].ptr = l4;
+            iov[m].len = (int32_t)l4len;
+            iov[m].start_sum = lvlip_pseudo_sum(le32(ih + 12), le32(ih + 16), PROTO_TCP,
+                                                (uint16_t)l4len) - le16(l4 + 16);
+            field[m++] = l4 + 16;
+        } else if (proto == PROTO_ICMP && l4len >= 4u) {
+            iov[m].ptr = l4;
+            iov[m].len = (int32_t)l4len;
+            iov[m].start_sum = 0u - le16(l4 + 2);
+            field[m++] = l4 + 2;
+        }
+        iov[m].ptr = ih;
+        iov[m].len = (int32_t)(ihl * 4u);
+        iov[m].start_sum = 0u - le16(ih + 10);
+        field[m++] = ih + 10;
+    }
+    return m;
+}
+
+void lvlip_tx_apply(uint32_t m, uint8_t *const *field, const uint16_t *csum)
+{
+    for (uint32_t k = 0; k < m; k++) memcpy(field[k], &csum[k], 2); /* raw store */
+}
+
+int lvlip_tx_checksum(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n)
+{
+    if (!ctx || (n && !frames)) return LVLIP_EINVAL;
+    if (n == 0) return LVLIP_OK;
+    /* validate every frame before touching any of them */
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t *h = frames[i].head;
+        if (!h || frames[i].len < ETH_HDR_LEN + 20u) return LVLIP_EINVAL;
+        const uint8_t *ih = h + ETH_HDR_LEN;
+        const uint32_t ihl = ih[0] & 0x0fu, iplen = be16(ih + 2);
+        if ((ih[0] >> 4) != 4u || ihl < 5u || iplen < ihl * 4u ||
+            frames[i].len < ETH_HDR_LEN + iplen)
+            return LVLIP_EINVAL;
+    }
+    lvlip_csum_iov *iov = (lvlip_csum_iov *)malloc(sizeof(lvlip_csum_iov) * 2u * (size_t)n);
+    uint8_t **field = (uint8_t **)malloc(sizeof(uint8_t *) * 2u * (size_t)n);
+    uint16_t *cs = (uint16_t *)malloc(sizeof(uint16_t) * 2u * (size_t)n);
+    int rc = LVLIP_ENOMEM;
+    if (iov && field && cs) {
+        const uint32_t m = lvlip_tx_plan(frames, n, iov, field);
+        rc = lvlip_csum_batch_host(ctx, iov, m, cs);
+        if (rc == LVLIP_OK) lvlip_tx_apply(m, field, cs);
+    }
+    free(iov);
+    free(field);
+    free(cs);
+    return rc;
+}

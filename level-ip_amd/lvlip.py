@@ -64,6 +64,16 @@ class Iov(ctypes.Structure):
     _fields_ = [("ptr", ctypes.c_void_p), ("len", ctypes.c_int32), ("start_sum", ctypes.c_uint32)]
 
 
+class Frame(ctypes.Structure):  # include/lvlip_skb.h: lvlip_frame
+    _fields_ = [("head", ctypes.c_void_p), ("len", ctypes.c_uint32)]
+
+
+# RX verdicts and flags (include/lvlip_skb.h)
+RX_OK, RX_NOT_IP, RX_SHORT, RX_BAD_VERSION, RX_BAD_IHL, RX_TTL0, RX_BAD_CSUM, RX_BAD_L4 = range(1, 9)
+RX_VERIFY_L4 = 0x1
+PLAN_MALFORMED = 0xFFFFFFFF
+
+
 def _share_torch_hip_runtime() -> None:
     """Make this process use ONE HIP runtime.
 
@@ -115,6 +125,19 @@ SIGNATURES = {
                                                   ctypes.c_void_p, ctypes.c_uint32,
                                                   ctypes.c_void_p]),
     "lvlip_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    # include/lvlip_skb.h (f1/f2 frame batches)
+    "lvlip_rx_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Frame), ctypes.c_uint32,
+                                       ctypes.c_uint32, ctypes.c_void_p]),
+    "lvlip_rx_plan": (ctypes.c_uint32, [ctypes.POINTER(Frame), ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.POINTER(Iov), ctypes.c_void_p]),
+    "lvlip_rx_apply": (None, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                              ctypes.c_void_p]),
+    "lvlip_tx_checksum": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Frame), ctypes.c_uint32]),
+    "lvlip_tx_plan": (ctypes.c_uint32, [ctypes.POINTER(Frame), ctypes.c_uint32, ctypes.POINTER(Iov),
+                                        ctypes.c_void_p]),
+    "lvlip_tx_apply": (None, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "lvlip_pseudo_sum_rfc": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8,
+                                               ctypes.c_uint16]),
     "lvlip_abi_version": (ctypes.c_int, []),
     "lvlip_device_count": (ctypes.c_int, []),
     "lvlip_last_hip_error": (ctypes.c_char_p, []),
@@ -218,6 +241,76 @@ def device_count() -> int:
     return int(_lib.lvlip_device_count())
 
 
+# ------------------------------------------------------------ frame batches --
+
+def frames_array(frames: Sequence[bytearray]):
+    """lvlip_frame[n] over writable buffers (bytearray / uint8 ndarray), in place.
+
+    Returns (array, keep); keep holds the buffer views alive while C uses them."""
+    n = len(frames)
+    arr = (Frame * max(n, 1))()
+    keep = []
+    for i, f in enumerate(frames):
+        if isinstance(f, np.ndarray):
+            a = f.view(np.uint8).reshape(-1)
+            if not a.flags.c_contiguous:
+                raise ValueError("frames must be contiguous")
+            ptr, ln = a.ctypes.data, a.size
+            keep.append(a)
+        else:
+            ln = len(f)
+            c = (ctypes.c_char * max(ln, 1)).from_buffer(f) if ln else None
+            ptr = ctypes.addressof(c) if c is not None else None
+            keep.append(c)
+        arr[i].head = ptr
+        arr[i].len = ln
+    return arr, keep
+
+
+def pseudo_sum_rfc(saddr: int, daddr: int, proto: int, length: int) -> int:
+    return int(_lib.lvlip_pseudo_sum_rfc(saddr & 0xFFFFFFFF, daddr & 0xFFFFFFFF, proto & 0xFF,
+                                         length & 0xFFFF))
+
+
+def rx_plan(frames, flags: int = 0):
+    """lvlip_rx_plan: (verdict[n] uint8, [(ptr, len, start_sum)] * m, tag[m] uint32)."""
+    n = len(frames)
+    arr, keep = frames_array(frames)
+    verdict = np.zeros(max(n, 1), dtype=np.uint8)
+    iov = (Iov * max(2 * n, 1))()
+    tag = np.zeros(max(2 * n, 1), dtype=np.uint32)
+    m = _lib.lvlip_rx_plan(arr, n, flags, verdict.ctypes.data, iov, tag.ctypes.data)
+    del keep
+    return verdict[:n], [(iov[k].ptr, iov[k].len, iov[k].start_sum) for k in range(m)], tag[:m]
+
+
+def rx_apply(verdict: np.ndarray, tag: np.ndarray, csum: np.ndarray) -> np.ndarray:
+    v = np.ascontiguousarray(verdict, dtype=np.uint8).copy()
+    t = np.ascontiguousarray(tag, dtype=np.uint32)
+    c = np.ascontiguousarray(csum, dtype=np.uint16)
+    _lib.lvlip_rx_apply(v.size, v.ctypes.data, t.size, t.ctypes.data, c.ctypes.data)
+    return v
+
+
+def tx_plan(frames):
+    """lvlip_tx_plan: ([(ptr, len, start_sum)] * m, field pointers[m]) or None if malformed."""
+    n = len(frames)
+    arr, keep = frames_array(frames)
+    iov = (Iov * max(2 * n, 1))()
+    field = np.zeros(max(2 * n, 1), dtype=np.uint64)
+    m = _lib.lvlip_tx_plan(arr, n, iov, field.ctypes.data)
+    del keep
+    if m == PLAN_MALFORMED:
+        return None
+    return [(iov[k].ptr, iov[k].len, iov[k].start_sum) for k in range(m)], field[:m].copy()
+
+
+def tx_apply(field: np.ndarray, csum: np.ndarray) -> None:
+    f = np.ascontiguousarray(field, dtype=np.uint64)
+    c = np.ascontiguousarray(csum, dtype=np.uint16)
+    _lib.lvlip_tx_apply(f.size, f.ctypes.data, c.ctypes.data)
+
+
 # ------------------------------------------------------------ host batches --
 
 class Context:
@@ -268,6 +361,22 @@ class Context:
                                                descs.ctypes.data, n, out.ctypes.data),
                "lvlip_csum_batch_host_flat")
         return out
+
+    def rx_verify(self, frames, flags: int = 0) -> np.ndarray:
+        """lvlip_rx_verify (f1): one verdict per frame (RX_*), frames untouched."""
+        n = len(frames)
+        arr, keep = frames_array(frames)
+        verdict = np.zeros(max(n, 1), dtype=np.uint8)
+        _check(_lib.lvlip_rx_verify(self._h, arr, n, flags, verdict.ctypes.data),
+               "lvlip_rx_verify")
+        del keep
+        return verdict[:n]
+
+    def tx_checksum(self, frames) -> None:
+        """lvlip_tx_checksum (f2): fills TCP/ICMP and IPv4 checksums in place."""
+        arr, keep = frames_array(frames)
+        _check(_lib.lvlip_tx_checksum(self._h, arr, len(frames)), "lvlip_tx_checksum")
+        del keep
 
 
 # ------------------------------------------------------------------ testkit --

@@ -183,3 +183,33 @@ def to_device(b: Batch, device="cuda", seed: int = SEED, stream=None):
             raise RuntimeError(f"testkit paint failed: {rc}")
     out = torch.empty(b.n, dtype=torch.int16, device=device)
     return base, descs, out
+
+
+# ------------------------------------------------------------------ frames --
+
+def frames(n: int, seed: int = SEED, max_l4: int = 1480, options: bool = True,
+           protos=(6, 1)) -> list[bytearray]:
+    """n Ethernet/IPv4 frames as level-ip builds them (include/skbuff.h:9-23):
+    14-B Ethernet header, IPv4 header (ihl 5, or up to 15 with options), then a
+    TCP (>= 20 B) or ICMP (>= 8 B) segment of random, often odd, length.  Every
+    checksum field holds garbage; bytes past the IP total length (Ethernet
+    padding) are random too.  Used by the f1/f2 tests (include/lvlip_skb.h)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        proto = int(rng.choice(protos))
+        ihl = int(rng.integers(6, 16)) if options and rng.random() < 0.2 else 5
+        lo = 20 if proto == 6 else 8
+        l4 = int(rng.integers(lo, max(lo, max_l4) + 1))
+        pad = int(rng.integers(0, 8)) if rng.random() < 0.3 else 0
+        iplen = ihl * 4 + l4
+        f = bytearray(rng.integers(0, 256, 14 + iplen + pad, dtype=np.uint8).tobytes())
+        f[12:14] = b"\x08\x00"
+        f[14] = 0x40 | ihl
+        f[16:18] = iplen.to_bytes(2, "big")
+        f[22] = int(rng.integers(1, 256))  # ttl != 0
+        f[23] = proto
+        if proto == 1:
+            f[14 + ihl * 4] = 8  # echo request
+        out.append(f)
+    return out

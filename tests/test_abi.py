@@ -12,12 +12,14 @@ import lvlip
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "lvlip_csum.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "lvlip_skb.h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    names = re.findall(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\(", src, flags=re.M)
+    names = []
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names += re.findall(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\(", src, flags=re.M)
     return sorted(set(n for n in names if n not in ("defined",)))
 
 
@@ -47,13 +49,15 @@ def test_every_declared_symbol_is_exported():
 
 def test_header_is_plain_c():
     # compiles as C99 with no HIP/torch headers on the include path
-    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c", "-"],
-                       input=f'#include "{HEADER}"\nint main(void){{return 0;}}\n', text=True,
-                       capture_output=True)
-    assert r.returncode == 0, r.stderr
-    body = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
-    assert not re.search(r"\bhip\w*_t\b|#include\s*<hip", body)
-    assert "torch" not in body.lower()
+    for h in HEADERS:
+        r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only",
+                            "-I", os.path.dirname(h), "-x", "c", "-"],
+                           input=f'#include "{h}"\nint main(void){{return 0;}}\n', text=True,
+                           capture_output=True)
+        assert r.returncode == 0, r.stderr
+        body = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        assert not re.search(r"\bhip\w*_t\b|#include\s*<hip", body)
+        assert "torch" not in body.lower()
 
 
 def test_desc_layout():

@@ -1,0 +1,105 @@
+"""f1/f2 on the GPU: lvlip_rx_verify / lvlip_tx_checksum (include/lvlip_skb.h)
+run their checksums as one GPU batch; every frame is compared with the
+oracle's restatement of the reference's RX/TX decisions (oracle/skb_oracle.py)
+and, for config #1, with the reference stack's own echo replies."""
+import numpy as np
+import pytest
+
+import golden_io
+import lvlip
+import skb_oracle
+import workloads
+from test_skb_cpu import _rx_cases
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available() or lvlip.device_count() == 0:
+        pytest.fail("GPU tests need a HIP device (run them on the MI355X box)")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    with lvlip.Context(0, arena_bytes=4 << 20) as c:
+        yield c
+
+
+def test_tx_checksum_frames(ctx):
+    fr = workloads.frames(5000, seed=31)
+    want = [bytearray(f) for f in fr]
+    for f in want:
+        skb_oracle.tx_fill(f)
+    ctx.tx_checksum(fr)
+    bad = [i for i, (a, b) in enumerate(zip(fr, want)) if bytes(a) != bytes(b)]
+    assert not bad, bad[:10]
+
+
+def test_tx_checksum_jumbo_and_tiny(ctx):
+    fr = workloads.frames(300, seed=32, max_l4=9000 - 60) + workloads.frames(300, seed=33, max_l4=8)
+    want = [bytearray(f) for f in fr]
+    for f in want:
+        skb_oracle.tx_fill(f)
+    ctx.tx_checksum(fr)
+    assert [bytes(f) for f in fr] == [bytes(f) for f in want]
+
+
+def test_tx_echo_reply_golden(ctx):
+    e = golden_io.echo()["echo"]
+    fr = []
+    for case in e:
+        rep = bytearray(bytes.fromhex(case["reply_hex"]))
+        rep[24:26] = b"\x00\x00"
+        rep[36:38] = b"\xff\xff"
+        fr.append(rep)
+    ctx.tx_checksum(fr)
+    assert [bytes(f) for f in fr] == [bytes.fromhex(c["reply_hex"]) for c in e]
+
+
+def test_tx_malformed_untouched(ctx):
+    fr = workloads.frames(10, seed=34, max_l4=200)
+    fr[7][14] = 0x35  # version 3
+    before = [bytes(f) for f in fr]
+    with pytest.raises(lvlip.LvlipError) as ei:
+        ctx.tx_checksum(fr)
+    assert ei.value.rc == lvlip.EINVAL
+    assert [bytes(f) for f in fr] == before
+
+
+def test_rx_verify_matches_ip_rcv(ctx):
+    fr = _rx_cases(41) + _rx_cases(42)
+    before = [bytes(f) for f in fr]
+    for flags in (0, lvlip.RX_VERIFY_L4):
+        got = ctx.rx_verify(fr, flags)
+        want = [skb_oracle.rx_verdict(f, flags) for f in fr]
+        assert got.tolist() == want, flags
+    assert [bytes(f) for f in fr] == before
+
+
+def test_rx_verify_large_batch(ctx):
+    """A batch bigger than the arena: valid TX output verifies OK (header), and
+    flipped bytes are caught exactly where the oracle catches them."""
+    fr = workloads.frames(20000, seed=43, max_l4=1460)
+    ctx.tx_checksum(fr)
+    rng = np.random.default_rng(44)
+    for i in rng.choice(len(fr), 2000, replace=False):
+        f = fr[int(i)]
+        f[14 + int(rng.integers(0, len(f) - 14))] ^= 0x10
+    for flags in (0, lvlip.RX_VERIFY_L4):
+        got = ctx.rx_verify(fr, flags)
+        want = np.array([skb_oracle.rx_verdict(f, flags) for f in fr], dtype=np.uint8)
+        assert np.array_equal(got, want), flags
+
+
+def test_rx_echo_requests_ok(ctx):
+    e = golden_io.echo()["echo"]
+    fr = [bytearray(bytes.fromhex(c["request_hex"])) for c in e]
+    assert ctx.rx_verify(fr, lvlip.RX_VERIFY_L4).tolist() == [lvlip.RX_OK] * len(fr)
+
+
+def test_empty(ctx):
+    assert ctx.rx_verify([], 0).size == 0
+    ctx.tx_checksum([])
