@@ -675,16 +675,19 @@ __global__ __launch_bounds__(FLAT_T) void k_flat(const uint8_t* __restrict__ bas
 // packet's first chunk in a head bitmap, kept per 64-chunk group with the
 // number of heads before the group.  Phase 2 sweeps the chunk space, one group
 // of 64 chunks per wave-load, U groups in flight per wave:
-//   rank   = heads before the group + v_mbcnt(heads below this lane) + own bit - 1
+//   rank   = heads before the group + heads at or below this lane - 1
 //            (no search: the packet of every lane in two mbcnt instructions),
 //   bytes  = whole 16-B aligned chunks from the packet's own address
 //            (coalesced across packet boundaries), odd-address packets
 //            byte-swapped within u16 halves (v_perm); no per-lane masking:
-//            phase 1 seeds each packet's accumulator with minus the sum of the
-//            bytes of its first/last chunk that lie outside it (mod 2^32),
-//   reduce = inclusive DPP prefix sum over the wave; each segment's tail lane
-//            takes P(tail) - P(head-1) and adds it to the packet's u32
-//            accumulator in LDS (mod-2^32 adds: exact in any order).
+//            a packet's first and last chunk, when they hold bytes outside
+//            it, are also stashed raw in LDS, and phase 4 subtracts those
+//            bytes once per packet (mod 2^32) — every byte is read from HBM
+//            once, by the sweep,
+//   reduce = inclusive DPP prefix sum P over the wave; a packet's first-chunk
+//            lane adds val - P and its last-chunk lane (or lane 63) adds P to
+//            the packet's u32 accumulator in LDS (mod-2^32 adds: exact in any
+//            order), which leaves each segment's sum there.
 // Packets longer than FCAP chunks go to a whole-wave loop instead.
 constexpr int FT = 256;                  // descriptors per tile = threads
 constexpr uint32_t FCAP = 128;           // chunks of the largest swept packet (2 KiB)
@@ -743,6 +746,7 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
     __shared__ uint4 s_grp[FGROUPS];   // by 64-chunk group: {heads lo, heads hi, heads before, 0}
     __shared__ uint32_t s_acc[FT];     // by descriptor
     __shared__ uint32_t s_big[FT];     // descriptors longer than FCAP chunks
+    __shared__ uint4 s_edge[2 * FT];   // by descriptor: raw first / last chunk
     __shared__ uint32_t s_tmp[8];
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
@@ -751,7 +755,7 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
     const uint32_t i_me = tile0 + t;
 
     // ---- phase 1: descriptors -> chunk counts, ranks, records, head bitmap
-    uint32_t start_sum = 0, nch = 0, meta = 0, corr = 0;
+    uint32_t start_sum = 0, nch = 0, meta = 0, lo = 0, lastv = 16;
     uint64_t a0 = 0;
     bool big = false;
     if (i_me < n) {
@@ -760,39 +764,21 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
         if (d.len > 0) {
             const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
             a0 = abs & ~15ull;
-            const uint32_t lo = (uint32_t)(abs & 15ull);
+            lo = (uint32_t)(abs & 15ull);
             const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
             const uint64_t c64 = (span + 15u) >> 4;
-            const uint32_t lastv = (uint32_t)(span - 16ull * (c64 - 1u));
+            lastv = (uint32_t)(span - 16ull * (c64 - 1u));
             const bool odd = abs & 1ull;
             big = c64 > FCAP;
             nch = big ? 0u : (uint32_t)c64;
-            meta = ((uint32_t)odd << 9) | (t << 18);
-            if (!big && (lo != 0u || lastv != 16u)) {
-                // The sweep sums whole 16-B chunks; subtract here, once per packet,
-                // the bytes of the first and last chunk that lie outside it (same
-                // parity convention, mod 2^32 — exact).
-                const uint4 f = load_global(a0);
-                const int fb1 = (c64 == 1u) ? (int)lastv : 16;
-                uint4 out_f = f;  // bytes of the first chunk outside [lo, fb1)
-                out_f.x &= ~byte_range_mask((int)lo, fb1, 0);
-                out_f.y &= ~byte_range_mask((int)lo, fb1, 1);
-                out_f.z &= ~byte_range_mask((int)lo, fb1, 2);
-                out_f.w &= ~byte_range_mask((int)lo, fb1, 3);
-                uint32_t c = odd ? chunk_words<true>(out_f) : chunk_words<false>(out_f);
-                if (c64 > 1u && lastv != 16u) {
-                    uint4 out_l = load_global(a0 + 16ull * (c64 - 1u));
-                    out_l.x &= ~byte_range_mask(0, (int)lastv, 0);
-                    out_l.y &= ~byte_range_mask(0, (int)lastv, 1);
-                    out_l.z &= ~byte_range_mask(0, (int)lastv, 2);
-                    out_l.w &= ~byte_range_mask(0, (int)lastv, 3);
-                    c += odd ? chunk_words<true>(out_l) : chunk_words<false>(out_l);
-                }
-                corr = c;
-            }
+            // edge flags: the sweep stashes the packet's first (bit 10) and last
+            // (bit 11) chunk in LDS when they hold bytes outside the packet
+            const bool ef = !big && (lo != 0u || (c64 == 1u && lastv != 16u));
+            const bool el = !big && c64 > 1u && lastv != 16u;
+            meta = nch | ((uint32_t)odd << 9) | ((uint32_t)ef << 10) | ((uint32_t)el << 11) | (t << 18);
         }
     }
-    s_acc[t] = 0u - corr;
+    s_acc[t] = 0u;
     for (uint32_t g = t; g < FGROUPS; g += FT) s_grp[g] = make_uint4(0u, 0u, 0u, 0u);
     uint32_t nbig = 0;
     const uint32_t big_pos = block_excl_scan(big ? 1u : 0u, s_tmp, &nbig);
@@ -823,13 +809,22 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
 
     // ---- phase 2: sweep the chunk space, groups wid, wid+4, ... ; U per round.
     // Every round issues exactly U loads, unconditionally (lanes past the chunk
-    // space read a valid chunk of the tile's first packet and are zeroed), after
+    // space read a valid chunk of the tile's last packet and are zeroed), after
     // all U group headers and all U records are in registers: hipcc then retires
     // them with counted vmcnt waits instead of draining.
+    //
+    // Segment sums without locating heads: with P the inclusive prefix over the
+    // wave, a packet's segment in a group is P(last lane) - (P(first lane) -
+    // val(first lane)).  So the lane holding the packet's first chunk adds
+    // val - P, the lane holding its last chunk (or lane 63) adds P, and a
+    // segment that starts at lane 0 as a continuation needs nothing (exclusive
+    // prefix 0).  One LDS atomic per group carries both.
     if (C > 0) {
         for (uint32_t gr = wid; gr < G; gr += 4u * U) {
             uint4 x[U];
-            uint32_t mt[U], hlo[U], hhi[U], hb[U], r[U];
+            uint32_t mt[U], kk[U];
+            bool vl[U];
+            uint32_t hlo[U], hhi[U], hb[U];
             bool gv[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -840,12 +835,16 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
                 hhi[u] = uniform(gg.y);
                 hb[u] = uniform(gg.z);
             }
+            uint32_t r[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t j = (gr + 4u * u) * 64u + lane;
-                const uint32_t excl = __builtin_amdgcn_mbcnt_hi(hhi[u], __builtin_amdgcn_mbcnt_lo(hlo[u], 0u));
-                const uint32_t own = (uint32_t)((((uint64_t)hhi[u] << 32) | hlo[u]) >> lane) & 1u;
-                r[u] = (gv[u] && j < C) ? hb[u] + excl + own - 1u : 0u;
+                // heads at or below this lane = bit 0 + heads of bits 1..lane
+                // = bit 0 + mbcnt(H >> 1); the scalar part folds into one add
+                const uint64_t H = ((uint64_t)hhi[u] << 32) | hlo[u];
+                const uint64_t Hs = H >> 1;
+                const uint32_t cnt = __builtin_amdgcn_mbcnt_hi((uint32_t)(Hs >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)Hs, 0u));
+                r[u] = (hb[u] + (uint32_t)(H & 1ull) - 1u) + cnt;  // always a valid rank
             }
             uint4 rec[U];
 #pragma unroll
@@ -853,21 +852,18 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t j = (gr + 4u * u) * 64u + lane;
-                const bool valid = gv[u] && j < C;
-                const uint32_t k = valid ? j - rec[u].z : 0u;
-                x[u] = load_nt_global((((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * k);
+                vl[u] = gv[u] && j < C;
+                kk[u] = vl[u] ? j - rec[u].z : 0u;
+                x[u] = load_nt_global((((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * kk[u]);
                 mt[u] = rec[u].w;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (!gv[u]) break;  // uniform
-                const uint32_t j = (gr + 4u * u) * 64u + lane;
-                const bool valid = j < C;
                 uint4 v = x[u];
                 const uint32_t m = mt[u];
-                const bool odd = valid && (m & (1u << 9));
-                if (__builtin_amdgcn_ballot_w64(odd)) {
-                    const uint32_t sel = odd ? 0x02030001u : 0x03020100u;
+                if (__builtin_amdgcn_ballot_w64((m & (1u << 9)) != 0u)) {
+                    const uint32_t sel = (m & (1u << 9)) ? 0x02030001u : 0x03020100u;
                     v.x = __builtin_amdgcn_perm(v.x, v.x, sel);
                     v.y = __builtin_amdgcn_perm(v.y, v.y, sel);
                     v.z = __builtin_amdgcn_perm(v.z, v.z, sel);
@@ -878,17 +874,15 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
                 val = dot2_acc(v.y, val);
                 val = dot2_acc(v.z, val);
                 val = dot2_acc(v.w, val);
-                if (!valid) val = 0;
+                val = vl[u] ? val : 0u;
                 const uint32_t P = wave_incl_scan(val);
-                // segment of this lane: from the last head at or below it (or lane 0)
-                const uint64_t H = (((uint64_t)hhi[u] << 32) | hlo[u]) | 1ull;
-                const uint64_t below = (lane == 63u) ? ~0ull : ((2ull << lane) - 1ull);
-                const uint32_t h = 63u - (uint32_t)__clzll(H & below);
-                const uint32_t Ph = (uint32_t)__shfl((int)P, (int)(h == 0u ? 0u : h - 1u), 64);
-                const uint32_t seg = P - (h == 0u ? 0u : Ph);
-                const bool next_head = (lane < 63u) && ((H >> (lane + 1u)) & 1ull);
-                const bool tail = valid && (lane == 63u || j + 1u == C || next_head);
-                if (tail) atomicAdd(&s_acc[m >> 18], seg);
+                const bool first = kk[u] == 0u;
+                const bool last = kk[u] + 1u == (m & 0xFFu);
+                const uint32_t add = (first ? val - P : 0u) + ((last || lane == 63u) ? P : 0u);
+                if (vl[u] && (first || last || lane == 63u)) atomicAdd(&s_acc[m >> 18], add);
+                // edge chunks, raw, for the corrections of phase 4 (no second read)
+                if (vl[u] && first && (m & (1u << 10))) s_edge[2u * (m >> 18)] = x[u];
+                if (vl[u] && last && (m & (1u << 11))) s_edge[2u * (m >> 18) + 1u] = x[u];
             }
         }
     }
@@ -910,8 +904,36 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
     }
     __syncthreads();
 
-    // ---- phase 4: fold and store (coalesced 2-B stores)
-    if (i_me < n) out[i_me] = finish(start_sum, s_acc[t]);
+    // ---- phase 4: edge corrections, fold and store (coalesced 2-B stores).
+    // The sweep summed whole 16-B chunks; subtract, once per packet, the bytes
+    // of its first and last chunk that lie outside it (same parity convention,
+    // mod 2^32 — exact).
+    if (i_me < n) {
+        uint32_t acc = s_acc[t];
+        if (meta & (3u << 10)) {
+            const bool odd = meta & (1u << 9);
+            uint32_t c = 0;
+            if (meta & (1u << 10)) {
+                uint4 f = s_edge[2u * t];
+                const int fb1 = (nch == 1u) ? (int)lastv : 16;
+                f.x &= ~byte_range_mask((int)lo, fb1, 0);
+                f.y &= ~byte_range_mask((int)lo, fb1, 1);
+                f.z &= ~byte_range_mask((int)lo, fb1, 2);
+                f.w &= ~byte_range_mask((int)lo, fb1, 3);
+                c += odd ? chunk_words<true>(f) : chunk_words<false>(f);
+            }
+            if (meta & (1u << 11)) {
+                uint4 l = s_edge[2u * t + 1u];
+                l.x &= ~byte_range_mask(0, (int)lastv, 0);
+                l.y &= ~byte_range_mask(0, (int)lastv, 1);
+                l.z &= ~byte_range_mask(0, (int)lastv, 2);
+                l.w &= ~byte_range_mask(0, (int)lastv, 3);
+                c += odd ? chunk_words<true>(l) : chunk_words<false>(l);
+            }
+            acc -= c;
+        }
+        out[i_me] = finish(start_sum, acc);
+    }
 }
 }  // namespace lvlip
 

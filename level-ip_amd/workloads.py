@@ -151,6 +151,11 @@ CONFIGS = {
     "tcp9000": lambda first=0, n=1 << 20: uniform(n, 9000, first, name="tcp9000"),
     "mixed": lambda first=0, n=1 << 21: mixed(n, first),
 }
+# layout variants of configs[1] for the lab scripts (slot stride: packed,
+# 128-B lines, 2 KiB NIC-style buffers); not bench workloads
+for _st in (1500, 1536, 2048):
+    CONFIGS[f"tcp1500_s{_st}"] = (lambda st: lambda first=0, n=1 << 20: uniform(
+        n, 1500, first, stride=st, name=f"tcp1500_s{st}"))(_st)
 
 
 def make(name: str, n: int | None = None, first: int = 0) -> Batch:

@@ -25,7 +25,7 @@ def counters(path):
 
 
 c = {}
-for sub in ("sq", "fetch", "write"):
+for sub in ("sq", "sq2", "fetch", "write"):
     p = os.path.join(prof, sub, f"{sub}_counter_collection.csv")
     if os.path.exists(p):
         c.update(counters(p))

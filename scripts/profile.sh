@@ -4,6 +4,7 @@
 #   2. SQ instruction / wait counters (own pass)          -> gpurun_out/prof/sq
 #   3. FETCH_SIZE (own pass; gfx950 reports 1/2 of wide streaming reads)
 #   4. WRITE_SIZE (own pass)
+#   (optional) SQ2="..." a second SQ counter pass, before 3
 # Each pass runs under its own time limit; anything but success/plain failure
 # (rc 0/1) stops the script.
 set -u
@@ -22,6 +23,7 @@ run() {  # name, rocprof args...
 }
 run trace --kernel-trace --stats -T
 run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-include-regex "$KRE" -T
+if [ -n "${SQ2:-}" ]; then run sq2 --pmc $SQ2 --kernel-include-regex "$KRE" -T; fi
 run fetch --pmc FETCH_SIZE --kernel-include-regex "$KRE" -T
 run write --pmc WRITE_SIZE --kernel-include-regex "$KRE" -T
 find $OUT -name "*.csv" | sort
