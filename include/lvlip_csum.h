@@ -68,6 +68,26 @@ uint16_t checksum(void *addr, int count, int start_sum);
 uint32_t lvlip_pseudo_sum(uint32_t saddr, uint32_t daddr, uint8_t proto,
                           uint16_t len);
 
+/* The reference's own wrappers around checksum(), kept with their signatures
+ * so a build that links this library in place of src/utils.c + these
+ * functions sees the same symbols. */
+struct sk_buff;
+struct iphdr;
+
+/* src/tcp.c:87-98: checksum(data, len, lvlip_pseudo_sum(saddr, daddr, proto, len)). */
+int tcp_udp_checksum(uint32_t saddr, uint32_t daddr, uint8_t proto, uint8_t *data,
+                     uint16_t len);
+
+/* src/tcp.c:100-103: tcp_udp_checksum(saddr, daddr, 6, skb->data, skb->len).
+ * Reads skb->len and skb->data at the offsets struct sk_buff has in
+ * include/skbuff.h:9-23 on LP64 (40 and 72). */
+int tcp_v4_checksum(struct sk_buff *skb, uint32_t saddr, uint32_t daddr);
+
+/* src/ip_output.c:8-12: ihdr->csum = checksum(ihdr, ihdr->ihl * 4, 0), stored
+ * raw; like the reference it does not zero the field first (its callers do,
+ * src/ip_output.c:42,50). */
+void ip_send_check(struct iphdr *ihdr);
+
 /* ======================================================================= */
 /* Group 2: device-resident batches                                         */
 /* ======================================================================= */

@@ -12,6 +12,7 @@
  * wrap-around.  Accumulating the same words in 64 bits and truncating once is
  * the same value mod 2^32, so the result is identical for every count.
  */
+#include <stddef.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -74,4 +75,45 @@ uint32_t lvlip_pseudo_sum(uint32_t saddr, uint32_t daddr, uint8_t proto, uint16_
     sum += (uint32_t)(uint16_t)((uint16_t)proto << 8);
     sum += (uint32_t)(uint16_t)((len << 8) | (len >> 8));
     return sum;
+}
+
+/* src/tcp.c:87-98 */
+int tcp_udp_checksum(uint32_t saddr, uint32_t daddr, uint8_t proto, uint8_t *data, uint16_t len)
+{
+    return checksum(data, len, (int)lvlip_pseudo_sum(saddr, daddr, proto, len));
+}
+
+/* The leading fields of struct sk_buff, include/skbuff.h:9-23, as laid out on
+ * LP64: only len and data are read. */
+struct lvlip_sk_buff_abi {
+    void *list_next, *list_prev; /* struct list_head */
+    void *rt;
+    void *dev;
+    int refcnt;
+    uint16_t protocol;
+    uint32_t len;
+    uint32_t dlen;
+    uint32_t seq;
+    uint32_t end_seq;
+    uint8_t *end;
+    uint8_t *head;
+    uint8_t *data;
+    uint8_t *payload;
+};
+_Static_assert(offsetof(struct lvlip_sk_buff_abi, len) == 40, "sk_buff.len offset");
+_Static_assert(offsetof(struct lvlip_sk_buff_abi, data) == 72, "sk_buff.data offset");
+
+/* src/tcp.c:100-103 */
+int tcp_v4_checksum(struct sk_buff *skb, uint32_t saddr, uint32_t daddr)
+{
+    const struct lvlip_sk_buff_abi *s = (const struct lvlip_sk_buff_abi *)(const void *)skb;
+    return tcp_udp_checksum(saddr, daddr, 6, s->data, (uint16_t)s->len);
+}
+
+/* src/ip_output.c:8-12; ihl is the low nibble of byte 0 (include/ip.h:33-34) */
+void ip_send_check(struct iphdr *ihdr)
+{
+    uint8_t *h = (uint8_t *)(void *)ihdr;
+    const uint16_t c = checksum(h, (h[0] & 0x0f) * 4, 0);
+    memcpy(h + 10, &c, 2);
 }

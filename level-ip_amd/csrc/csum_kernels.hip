@@ -743,7 +743,8 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
                                               const lvlip_csum_desc* __restrict__ descs,
                                               uint32_t n, uint16_t* __restrict__ out) {
     __shared__ uint4 s_rec[FT];        // by rank: {a0 lo, a0 hi, cstart, meta}
-    __shared__ uint4 s_grp[FGROUPS];   // by 64-chunk group: {heads lo, heads hi, heads before, 0}
+    __shared__ uint2 s_grp[FGROUPS];   // by 64-chunk group: head bitmap {lo, hi}
+    __shared__ uint16_t s_hb[FGROUPS]; // by 64-chunk group: heads before it (<= FT)
     __shared__ uint32_t s_acc[FT];     // by descriptor
     __shared__ uint32_t s_big[FT];     // descriptors longer than FCAP chunks
     __shared__ uint4 s_edge[2 * FT];   // by descriptor: raw first / last chunk
@@ -779,7 +780,7 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
         }
     }
     s_acc[t] = 0u;
-    for (uint32_t g = t; g < FGROUPS; g += FT) s_grp[g] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t g = t; g < FGROUPS; g += FT) s_grp[g] = make_uint2(0u, 0u);
     uint32_t nbig = 0;
     const uint32_t big_pos = block_excl_scan(big ? 1u : 0u, s_tmp, &nbig);
     if (big) s_big[big_pos] = t;
@@ -802,8 +803,8 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
         const uint32_t p1 = g1 < G ? (uint32_t)__popcll(((uint64_t)s_grp[g1].y << 32) | s_grp[g1].x) : 0u;
         uint32_t tot = 0;
         const uint32_t before = block_excl_scan(p0 + p1, s_tmp, &tot);
-        if (g0 < G) s_grp[g0].z = before;
-        if (g1 < G) s_grp[g1].z = before + p0;
+        if (g0 < G) s_hb[g0] = (uint16_t)before;
+        if (g1 < G) s_hb[g1] = (uint16_t)(before + p0);
     }
     __syncthreads();
 
@@ -830,10 +831,11 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
             for (int u = 0; u < U; ++u) {
                 const uint32_t g = gr + 4u * u;
                 gv[u] = g < G;
-                const uint4 gg = s_grp[gv[u] ? g : G - 1u];
+                const uint32_t gc = gv[u] ? g : G - 1u;
+                const uint2 gg = s_grp[gc];
                 hlo[u] = uniform(gg.x);
                 hhi[u] = uniform(gg.y);
-                hb[u] = uniform(gg.z);
+                hb[u] = uniform((uint32_t)s_hb[gc]);
             }
             uint32_t r[U];
 #pragma unroll

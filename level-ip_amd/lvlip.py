@@ -111,6 +111,10 @@ SIGNATURES = {
     "checksum": (ctypes.c_uint16, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "lvlip_pseudo_sum": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8,
                                             ctypes.c_uint16]),
+    "tcp_udp_checksum": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8,
+                                        ctypes.c_void_p, ctypes.c_uint16]),
+    "tcp_v4_checksum": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]),
+    "ip_send_check": (None, [ctypes.c_void_p]),
     "lvlip_csum_batch_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                             ctypes.c_void_p, ctypes.c_void_p]),
     "lvlip_csum_batch_dev_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
@@ -194,14 +198,20 @@ def pseudo_sum(saddr: int, daddr: int, proto: int, length: int) -> int:
 def tcp_udp_checksum(saddr: int, daddr: int, proto: int, data, length: int) -> int:
     """src/tcp.c:87-98 (len is a uint16_t there, so it is truncated the same way)."""
     length &= 0xFFFF
-    return checksum(data, length, pseudo_sum(saddr, daddr, proto, length))
+    a = _as_u8(data)
+    if length > a.size:
+        raise ValueError("length exceeds buffer")
+    return int(_lib.tcp_udp_checksum(saddr & 0xFFFFFFFF, daddr & 0xFFFFFFFF, proto & 0xFF,
+                                     a.ctypes.data if a.size else None, length))
 
 
 def ip_send_check(hdr: bytearray) -> None:
     """src/ip_output.c:8-12: checksum over ihl*4 bytes, stored raw at offset 10."""
-    ihl = hdr[0] & 0x0F
-    c = checksum(bytes(hdr[: ihl * 4]), ihl * 4, 0)
-    hdr[10:12] = int(c).to_bytes(2, "little")
+    if len(hdr) < max(20, (hdr[0] & 0x0F) * 4):
+        raise ValueError("header shorter than ihl*4")
+    c = (ctypes.c_char * len(hdr)).from_buffer(hdr)
+    _lib.ip_send_check(ctypes.addressof(c))
+    del c
 
 
 # ---------------------------------------------------------- device batches --

@@ -1,10 +1,13 @@
 """Group 1 of include/lvlip_csum.h — the per-call drop-in for src/utils.c:22-55 —
 against the reference's outputs, plus BASELINE config #1 (ICMPv4 echo through
 the reference stack with a fake TAP, CPU only)."""
+import ctypes
+
 import numpy as np
 
 import golden_io
 import lvlip
+import pyoracle
 
 
 def test_kats():
@@ -84,3 +87,52 @@ def test_echo_config1_cpu():
         # and the full reply verifies
         assert lvlip.checksum(bytes(rep[14:34]), 20, 0) == 0
         assert lvlip.checksum(bytes(rep[34:14 + iplen]), iplen - 20, 0) == 0
+
+
+class SkBuff(ctypes.Structure):
+    # struct sk_buff, include/skbuff.h:9-23, LP64 (the layout tcp_v4_checksum reads)
+    _fields_ = [("next", ctypes.c_void_p), ("prev", ctypes.c_void_p), ("rt", ctypes.c_void_p),
+                ("dev", ctypes.c_void_p), ("refcnt", ctypes.c_int), ("protocol", ctypes.c_uint16),
+                ("len", ctypes.c_uint32), ("dlen", ctypes.c_uint32), ("seq", ctypes.c_uint32),
+                ("end_seq", ctypes.c_uint32), ("end", ctypes.c_void_p), ("head", ctypes.c_void_p),
+                ("data", ctypes.c_void_p), ("payload", ctypes.c_void_p)]
+
+
+def test_tcp_v4_checksum_skb():
+    """The exported tcp_v4_checksum (src/tcp.c:100-103) reads skb->data/len at
+    the reference's offsets: golden TCP vectors through an sk_buff, and (where
+    oracle/_ref is built) the reference's own tcp_v4_checksum on the same skb."""
+    assert ctypes.sizeof(SkBuff) == 88 and SkBuff.len.offset == 40 and SkBuff.data.offset == 72
+    t = golden_io.tcp()
+    ref = pyoracle.reflib()
+    if ref is not None:
+        ref.tcp_v4_checksum.restype = ctypes.c_int
+        ref.tcp_v4_checksum.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+    n = 0
+    for i in range(t["len"].size):
+        if int(t["proto"][i]) != 6:
+            continue
+        off, ln = int(t["offset"][i]), int(t["len"][i])
+        seg = np.ascontiguousarray(t["blob"][off:off + max(ln, 1)])
+        skb = SkBuff(len=ln, data=seg.ctypes.data, head=seg.ctypes.data, refcnt=1)
+        s, d = int(t["saddr"][i]), int(t["daddr"][i])
+        got = lvlip.lib().tcp_v4_checksum(ctypes.byref(skb), s, d)
+        assert got == int(t["expected"][i]), i
+        if ref is not None:
+            assert ref.tcp_v4_checksum(ctypes.byref(skb), s, d) == got, i
+        n += 1
+    assert n > 100
+
+
+def test_ip_send_check_symbol_matches_reference():
+    h = golden_io.iphdr()
+    ref = pyoracle.reflib()
+    for hdr in h["hdr"][:50]:
+        a = bytearray(hdr.tobytes())
+        b = bytearray(a)
+        lvlip.ip_send_check(a)
+        if ref is not None:
+            c = (ctypes.c_char * len(b)).from_buffer(b)
+            ref.ip_send_check(ctypes.addressof(c))
+            del c
+            assert a == b
