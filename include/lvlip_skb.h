@@ -91,6 +91,28 @@ uint32_t lvlip_tx_plan(lvlip_frame *frames, uint32_t n, lvlip_csum_iov *iov,
                        uint8_t **field);
 void lvlip_tx_apply(uint32_t m, uint8_t *const *field, const uint16_t *csum);
 
+/* ---- f4: RFC 1624 incremental update for the echo reply ----------------- */
+
+/* icmpv4_reply (src/icmpv4.c:44-47) turns an echo request into the reply by
+ * setting type 8 -> 0 and recomputing the ICMP checksum over the whole
+ * message.  Given the request's stored checksum field (raw u16, as loaded
+ * from the frame) of a request whose ICMP checksum VERIFIED (checksum over
+ * the message == 0, e.g. LVLIP_RX_OK from lvlip_rx_verify with
+ * LVLIP_RX_VERIFY_L4), returns the reply's checksum field, bit-identical to
+ * the reference's full recomputation, without reading the message; or
+ * LVLIP_CSUM_RECOMPUTE in the one case the field cannot decide (the reply's
+ * one's-complement sum is 0xffff, which is also what an all-zero reply
+ * gives), where the caller recomputes with checksum(). */
+#define LVLIP_CSUM_RECOMPUTE 0xFFFFFFFFu
+uint32_t lvlip_icmp_echo_reply_csum(uint16_t req_csum);
+
+/* In place over n verified echo-request frames: ICMP type 8 -> 0 and the
+ * checksum field updated as above (recomputed with checksum() in the
+ * undecidable case).  Returns the number of frames that needed the
+ * recomputation, or 0xFFFFFFFF (frames untouched) if one is not an ICMP echo
+ * request. */
+uint32_t lvlip_icmp_echo_reply_fill(lvlip_frame *frames, uint32_t n);
+
 /* RFC 1071 pseudo-header seed with the carries folded back (for RX verify of
  * checksums produced by RFC-correct peers). */
 uint32_t lvlip_pseudo_sum_rfc(uint32_t saddr, uint32_t daddr, uint8_t proto,

@@ -214,3 +214,58 @@ int lvlip_tx_checksum(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n)
     free(cs);
     return rc;
 }
+
+/* ----------------------------------------------------------------- f4: RFC 1624 */
+
+/* One's-complement add of two 16-bit values (end-around carry). */
+static inline uint32_t oc_add(uint32_t a, uint32_t b)
+{
+    const uint32_t t = a + b;
+    return (t & 0xffffu) + (t >> 16);
+}
+
+uint32_t lvlip_icmp_echo_reply_csum(uint16_t req_csum)
+{
+    /* The request verified: S + HC == 0xffff (one's complement), S the sum of the
+     * message with the field zeroed, S in [1, 0xffff] (its type byte is 8).  So
+     * S = ~HC, except HC = 0xffff (the other representation of zero), S = 0xffff.
+     * Reply: the word {type, code} = 0x0008 becomes 0x0000 (RFC 1624 eqn. 3:
+     * S' = S + ~m + m').  The reference's double fold of the full sum yields the
+     * same value in [1, 0xffff] for any non-zero message, and 0 only for an
+     * all-zero one; S' = 0xffff cannot tell those apart, hence RECOMPUTE. */
+    const uint32_t S = req_csum == 0xffffu ? 0xffffu : (uint32_t)(uint16_t)~req_csum;
+    const uint32_t S1 = oc_add(S, 0xffffu - 0x0008u);
+    if (S1 == 0xffffu) return LVLIP_CSUM_RECOMPUTE;
+    return (uint16_t)~S1;
+}
+
+uint32_t lvlip_icmp_echo_reply_fill(lvlip_frame *frames, uint32_t n)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t *h = frames[i].head;
+        if (!h || frames[i].len < ETH_HDR_LEN + 20u) return 0xFFFFFFFFu;
+        const uint8_t *ih = h + ETH_HDR_LEN;
+        const uint32_t ihl = ih[0] & 0x0fu, iplen = be16(ih + 2);
+        if ((ih[0] >> 4) != 4u || ihl < 5u || ih[9] != PROTO_ICMP || iplen < ihl * 4u + 4u ||
+            frames[i].len < ETH_HDR_LEN + iplen || ih[ihl * 4u] != 8u || ih[ihl * 4u + 1u] != 0u)
+            return 0xFFFFFFFFu;
+    }
+    uint32_t recomputed = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t *ih = frames[i].head + ETH_HDR_LEN;
+        const uint32_t ihl = ih[0] & 0x0fu, icmp_len = be16(ih + 2) - ihl * 4u;
+        uint8_t *icmp = ih + ihl * 4u;
+        const uint32_t c = lvlip_icmp_echo_reply_csum((uint16_t)le16(icmp + 2));
+        icmp[0] = 0; /* ICMP_V4_REPLY, src/icmpv4.c:45 */
+        uint16_t v;
+        if (c == LVLIP_CSUM_RECOMPUTE) {
+            memset(icmp + 2, 0, 2);
+            v = checksum(icmp, (int)icmp_len, 0); /* src/icmpv4.c:46-47 */
+            recomputed++;
+        } else {
+            v = (uint16_t)c;
+        }
+        memcpy(icmp + 2, &v, 2);
+    }
+    return recomputed;
+}

@@ -140,6 +140,8 @@ SIGNATURES = {
     "lvlip_tx_plan": (ctypes.c_uint32, [ctypes.POINTER(Frame), ctypes.c_uint32, ctypes.POINTER(Iov),
                                         ctypes.c_void_p]),
     "lvlip_tx_apply": (None, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "lvlip_icmp_echo_reply_csum": (ctypes.c_uint32, [ctypes.c_uint16]),
+    "lvlip_icmp_echo_reply_fill": (ctypes.c_uint32, [ctypes.POINTER(Frame), ctypes.c_uint32]),
     "lvlip_pseudo_sum_rfc": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8,
                                                ctypes.c_uint16]),
     "lvlip_abi_version": (ctypes.c_int, []),
@@ -313,6 +315,26 @@ def tx_plan(frames):
     if m == PLAN_MALFORMED:
         return None
     return [(iov[k].ptr, iov[k].len, iov[k].start_sum) for k in range(m)], field[:m].copy()
+
+
+CSUM_RECOMPUTE = 0xFFFFFFFF
+
+
+def icmp_echo_reply_csum(req_csum: int) -> int:
+    """f4 (RFC 1624): reply checksum field from a verified request's field, or
+    CSUM_RECOMPUTE."""
+    return int(_lib.lvlip_icmp_echo_reply_csum(req_csum & 0xFFFF))
+
+
+def icmp_echo_reply_fill(frames) -> int:
+    """In place: echo requests -> replies' ICMP part (type 0 + checksum).
+    Returns how many needed a full recomputation; raises on a non-request."""
+    arr, keep = frames_array(frames)
+    r = int(_lib.lvlip_icmp_echo_reply_fill(arr, len(frames)))
+    del keep
+    if r == PLAN_MALFORMED:
+        raise ValueError("not an ICMP echo request frame")
+    return r
 
 
 def tx_apply(field: np.ndarray, csum: np.ndarray) -> None:

@@ -225,3 +225,84 @@ def test_empty_batches():
     assert v.size == 0 and entries == [] and tag.size == 0
     entries, field = lvlip.tx_plan([])
     assert entries == [] and field.size == 0
+
+
+# ------------------------------------------------------------ f4: RFC 1624 --
+
+def _echo_request(payload: bytes, ident=0x1234, seq=1, alt_zero=False):
+    """Ethernet + IPv4 + ICMP echo request with a valid ICMP checksum (oracle)."""
+    icmp = bytearray(b"\x08\x00\x00\x00" + ident.to_bytes(2, "big") + seq.to_bytes(2, "big") + payload)
+    c = pyoracle.checksum(bytes(icmp), len(icmp), 0)
+    if alt_zero and c == 0:
+        c = 0xFFFF  # the other one's-complement zero: verifies too
+    icmp[2:4] = struct.pack("<H", c)
+    f = bytearray(14) + bytearray(20) + icmp
+    f[12:14] = b"\x08\x00"
+    f[14], f[22], f[23] = 0x45, 64, 1
+    f[16:18] = (20 + len(icmp)).to_bytes(2, "big")
+    skb_oracle.tx_fill(bytearray(f))  # (shape check only)
+    assert pyoracle.checksum(bytes(icmp), len(icmp), 0) == 0 or alt_zero
+    return f
+
+
+def _reply_full(frame: bytearray) -> bytes:
+    """src/icmpv4.c:44-47: type = 0, csum = 0, csum = checksum(icmp, icmp_len, 0)."""
+    g = bytearray(frame)
+    ihl = g[14] & 0xF
+    iplen = int.from_bytes(g[16:18], "big")
+    o = 14 + ihl * 4
+    g[o] = 0
+    g[o + 2:o + 4] = b"\0\0"
+    g[o + 2:o + 4] = struct.pack("<H", pyoracle.checksum(bytes(g[o:14 + iplen]), iplen - ihl * 4, 0))
+    return bytes(g)
+
+
+def test_icmp_incremental_random():
+    rng = np.random.default_rng(61)
+    frames = []
+    for _ in range(3000):
+        ln = int(rng.integers(0, 1473))
+        frames.append(_echo_request(rng.integers(0, 256, ln, dtype=np.uint8).tobytes(),
+                                    int(rng.integers(0, 1 << 16)), int(rng.integers(0, 1 << 16))))
+    want = [_reply_full(f) for f in frames]
+    n_re = lvlip.icmp_echo_reply_fill(frames)
+    assert [bytes(f) for f in frames] == want
+    assert n_re <= 3  # ~1/65535 per frame
+
+
+def test_icmp_incremental_edges():
+    cases = [
+        _echo_request(b"", ident=0, seq=0),                    # reply all zero: 0xffff
+        _echo_request(b"", ident=0xF7FF, seq=0),               # request sum 0xffff, field 0
+        _echo_request(b"", ident=0xF7FF, seq=0, alt_zero=True),  # same, field 0xffff
+        _echo_request(b"\xff\xff", ident=0, seq=0),            # reply sum 0xffff: 0x0000
+        _echo_request(b"\x00" * 64, ident=0, seq=0),
+        _echo_request(b"\xff" * 9, ident=0xFFFF, seq=0xFFFF),  # odd length
+    ]
+    assert cases[1][36:38] == b"\0\0" and cases[2][36:38] == b"\xff\xff"
+    want = [_reply_full(f) for f in cases]
+    assert lvlip.icmp_echo_reply_fill([bytearray(f) for f in cases]) == 3  # cases 0, 3, 4
+    lvlip.icmp_echo_reply_fill(cases)
+    assert [bytes(f) for f in cases] == want
+    assert int.from_bytes(want[0][36:38], "little") == 0xFFFF
+    assert lvlip.icmp_echo_reply_csum(0xFFF7) == lvlip.CSUM_RECOMPUTE
+
+
+def test_icmp_incremental_echo_golden():
+    """Config #1 requests -> the ICMP part of the replies the reference stack wrote."""
+    e = golden_io.echo()["echo"]
+    fr = [bytearray(bytes.fromhex(c["request_hex"])) for c in e]
+    lvlip.icmp_echo_reply_fill(fr)
+    for f, c in zip(fr, e):
+        rep = bytes.fromhex(c["reply_hex"])
+        iplen = int.from_bytes(rep[16:18], "big")
+        assert bytes(f[34:14 + iplen]) == rep[34:14 + iplen]
+
+
+def test_icmp_incremental_refuses_non_requests():
+    fr = [_echo_request(b"abc"), bytearray(workloads.frames(1, seed=62, protos=(6,))[0])]
+    before = [bytes(f) for f in fr]
+    import pytest
+    with pytest.raises(ValueError):
+        lvlip.icmp_echo_reply_fill(fr)
+    assert [bytes(f) for f in fr] == before
