@@ -178,6 +178,25 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx *ctx, const void *base,
                                size_t base_bytes, const lvlip_csum_desc *d,
                                uint32_t n, uint16_t *out);
 
+/* f3: zero-copy host staging.  Registers host memory that
+ * holds packets (an skb slab, a frame pool, a receive ring) with the context
+ * (hipHostRegister, whole pages pinned in place).  Batches whose bytes lie in
+ * one registered region skip the gather into the pinned arena:
+ *   LVLIP_REG_DMA       batch_host_flat copies each piece's span straight
+ *                       from the region with the copy engine (no CPU memcpy);
+ *                       batch_host (scattered packets) still gathers
+ *   LVLIP_REG_ZEROCOPY  the kernel reads the packets in place over PCIe: only
+ *                       descriptors go down and results come back, for
+ *                       batch_host (any packets inside the region) and
+ *                       batch_host_flat alike
+ * Regions must not overlap; the memory must stay valid until unregistered
+ * (lvlip_csum_ctx_destroy unregisters what is left).  Results are identical
+ * on every path. */
+#define LVLIP_REG_DMA      0u
+#define LVLIP_REG_ZEROCOPY 1u
+int lvlip_csum_register(lvlip_csum_ctx *ctx, void *ptr, size_t bytes, uint32_t flags);
+int lvlip_csum_unregister(lvlip_csum_ctx *ctx, void *ptr);
+
 /* ======================================================================= */
 /* Misc                                                                     */
 /* ======================================================================= */

@@ -50,6 +50,15 @@ struct Slot {
     bool busy = false;
 };
 
+// A registered host region (f3): pinned in place, mapped into the device's
+// address space.
+struct Region {
+    uint8_t* host = nullptr;
+    size_t bytes = 0;
+    uint8_t* dev = nullptr;  // device address of host[0]
+    uint32_t flags = 0;
+};
+
 }  // namespace
 
 struct lvlip_csum_ctx {
@@ -58,6 +67,7 @@ struct lvlip_csum_ctx {
     uint32_t max_desc = 0;  // descriptors per slot
     int threads = 1;        // host threads for the gather into the pinned arena
     Slot slot[kSlots];
+    std::vector<Region> regions;
     char err[256] = "";
 };
 
@@ -91,19 +101,27 @@ int drain(lvlip_csum_ctx* c, Slot& s) {
     return LVLIP_OK;
 }
 
-// Copy the gathered piece in `s` to the device, checksum it, copy results back.
-int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uint16_t* user_out) {
+// Copy a piece to the device, checksum it, copy results back.  The bytes come
+// from `src` (the slot's pinned arena, or a registered region: DMA straight
+// from it), or, when `dev_base` is set, are read by the kernel in place
+// (zero-copy: `bytes` is then only the length hint's numerator).
+int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uint16_t* user_out,
+                 const uint8_t* src = nullptr, const uint8_t* dev_base = nullptr) {
     hipError_t e;
-    if ((e = hipMemcpyAsync(s.d_bytes, s.h_bytes, align16(bytes), hipMemcpyHostToDevice,
-                            s.stream)) != hipSuccess)
-        return fail(c, e, "H2D bytes");
+    if (!dev_base) {
+        const uint64_t nb = src && src != s.h_bytes ? bytes : align16(bytes);
+        if ((e = hipMemcpyAsync(s.d_bytes, src ? src : s.h_bytes, nb, hipMemcpyHostToDevice,
+                                s.stream)) != hipSuccess)
+            return fail(c, e, "H2D bytes");
+    }
     if ((e = hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)count * sizeof(lvlip_csum_desc),
                             hipMemcpyHostToDevice, s.stream)) != hipSuccess)
         return fail(c, e, "H2D descriptors");
     lvlip_launch_cfg cfg{};
     cfg.kernel = LVLIP_KERNEL_AUTO;  // the piece's average length picks the kernel
     cfg.len_hint = (int32_t)(bytes / count > 0x7fffffffull ? 0x7fffffff : bytes / count);
-    int rc = lvlip_csum_batch_dev_ex(s.d_bytes, s.d_desc, count, s.d_out, s.stream, &cfg);
+    int rc = lvlip_csum_batch_dev_ex(dev_base ? dev_base : s.d_bytes, s.d_desc, count, s.d_out,
+                                     s.stream, &cfg);
     if (rc != LVLIP_OK) return rc;
     if ((e = hipMemcpyAsync(s.h_out, s.d_out, (size_t)count * sizeof(uint16_t),
                             hipMemcpyDeviceToHost, s.stream)) != hipSuccess)
@@ -143,6 +161,48 @@ void parallel_ranges(int threads, uint64_t n, uint64_t min_per_thread, F fn) {
         pool.emplace_back([=] { fn(n * k / t, n * (k + 1) / t); });
     fn(0, n / t);
     for (auto& th : pool) th.join();
+}
+
+// The registered region holding [p, p + len), or nullptr.
+const Region* find_region(const lvlip_csum_ctx* c, const void* p, uint64_t len) {
+    const uint8_t* a = (const uint8_t*)p;
+    for (const Region& r : c->regions)
+        if (a >= r.host && a + len <= r.host + r.bytes) return &r;
+    return nullptr;
+}
+
+// Zero-copy: descriptors only (offsets from the region's first byte rounded
+// down to 16), kernel reads the registered pages in place.  `offset_of(i)`
+// gives packet i's byte address; the whole batch lies in region `r`.
+template <class AddrOf, class DescOf>
+int zerocopy_batch(lvlip_csum_ctx* c, const Region& r, uint32_t n, uint16_t* out, AddrOf addr_of,
+                   DescOf desc_of) {
+    const uint8_t* h0 = (const uint8_t*)((uintptr_t)r.host & ~(uintptr_t)15);
+    const uint8_t* d0 = r.dev - (r.host - h0);
+    int cur = 0;
+    uint32_t i = 0;
+    int rc = LVLIP_OK;
+    while (i < n && rc == LVLIP_OK) {
+        Slot& s = c->slot[cur];
+        if ((rc = drain(c, s)) != LVLIP_OK) break;
+        const uint32_t first = i;
+        const uint32_t k = n - i < c->max_desc ? n - i : c->max_desc;
+        uint64_t bytes = 0;
+        for (uint32_t q = 0; q < k; ++q) {
+            lvlip_csum_desc dq = desc_of(first + q);
+            dq.offset = (uint64_t)((const uint8_t*)addr_of(first + q) - h0);
+            bytes += dq.len > 0 ? (uint64_t)dq.len : 0u;
+            s.h_desc[q] = dq;
+        }
+        i += k;
+        rc = launch_piece(c, s, bytes ? bytes : 16, k, out + first, nullptr, d0);
+        cur ^= 1;
+    }
+    for (auto& s : c->slot) {
+        const int r2 = drain(c, s);
+        if (rc == LVLIP_OK) rc = r2;
+    }
+    return rc;
 }
 
 }  // namespace
@@ -203,8 +263,47 @@ int lvlip_csum_ctx_destroy(lvlip_csum_ctx* c) {
         if (s.busy) (void)hipEventSynchronize(s.done);
         free_slot(s);
     }
+    for (const Region& r : c->regions) (void)hipHostUnregister(r.host);
     delete c;
     return LVLIP_OK;
+}
+
+int lvlip_csum_register(lvlip_csum_ctx* c, void* ptr, size_t bytes, uint32_t flags) {
+    if (!c || !ptr || bytes == 0 || flags > LVLIP_REG_ZEROCOPY) return LVLIP_EINVAL;
+    uint8_t* p = (uint8_t*)ptr;
+    for (const Region& r : c->regions)
+        if (p < r.host + r.bytes && r.host < p + bytes) return LVLIP_EINVAL;  // overlap
+    DeviceGuard g(c->device);
+    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterMapped);
+    if (e != hipSuccess) return fail(c, e, "hipHostRegister");
+    void* dev = nullptr;
+    if ((e = hipHostGetDevicePointer(&dev, ptr, 0)) != hipSuccess) {
+        (void)hipHostUnregister(ptr);
+        return fail(c, e, "hipHostGetDevicePointer");
+    }
+    Region r;
+    r.host = p;
+    r.bytes = bytes;
+    r.dev = (uint8_t*)dev;
+    r.flags = flags;
+    c->regions.push_back(r);
+    return LVLIP_OK;
+}
+
+int lvlip_csum_unregister(lvlip_csum_ctx* c, void* ptr) {
+    if (!c || !ptr) return LVLIP_EINVAL;
+    for (size_t k = 0; k < c->regions.size(); ++k) {
+        if (c->regions[k].host != (uint8_t*)ptr) continue;
+        DeviceGuard g(c->device);
+        for (auto& s : c->slot) {  // nothing in flight may still read it
+            const int rc = drain(c, s);
+            if (rc != LVLIP_OK) return rc;
+        }
+        const hipError_t e = hipHostUnregister(ptr);
+        c->regions.erase(c->regions.begin() + (long)k);
+        return e == hipSuccess ? LVLIP_OK : fail(c, e, "hipHostUnregister");
+    }
+    return LVLIP_EINVAL;
 }
 
 int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_t n,
@@ -212,9 +311,32 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
     if (!c || (n && (!pkts || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
     for (uint32_t i = 0; i < n; ++i)
-        if (pkts[i].len > 0 && (!pkts[i].ptr || align16((uint64_t)pkts[i].len) > c->arena))
-            return LVLIP_ERANGE;  // a single packet larger than the arena
+        if (pkts[i].len > 0 && !pkts[i].ptr) return LVLIP_EINVAL;
     DeviceGuard g(c->device);
+    if (!c->regions.empty()) {
+        // f3: all packets inside one zero-copy region -> no gather at all
+        const Region* r = nullptr;
+        uint32_t i = 0;
+        for (; i < n; ++i) {
+            if (pkts[i].len <= 0) continue;
+            const Region* ri = find_region(c, pkts[i].ptr, (uint64_t)pkts[i].len);
+            if (!ri || !(ri->flags & LVLIP_REG_ZEROCOPY) || (r && ri != r)) break;
+            r = ri;
+        }
+        if (i == n && r)
+            return zerocopy_batch(
+                c, *r, n, out,
+                [&](uint32_t q) { return pkts[q].len > 0 ? (const uint8_t*)pkts[q].ptr : r->host; },
+                [&](uint32_t q) {
+                    lvlip_csum_desc d{};
+                    d.len = pkts[q].len;
+                    d.start_sum = pkts[q].start_sum;
+                    return d;
+                });
+    }
+    for (uint32_t i = 0; i < n; ++i)
+        if (pkts[i].len > 0 && align16((uint64_t)pkts[i].len) > c->arena)
+            return LVLIP_ERANGE;  // a single packet larger than the arena
 
     int cur = 0;
     uint32_t i = 0;
@@ -262,7 +384,14 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
     if (!c || (n && (!base || !d || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
     const uint8_t* b = (const uint8_t*)base;
+    for (uint32_t q = 0; q < n; ++q)
+        if (d[q].offset + (d[q].len > 0 ? (uint64_t)d[q].len : 0u) > base_bytes) return LVLIP_EINVAL;
     DeviceGuard g(c->device);
+    const Region* reg = c->regions.empty() ? nullptr : find_region(c, b, base_bytes);
+    if (reg && (reg->flags & LVLIP_REG_ZEROCOPY))
+        return zerocopy_batch(
+            c, *reg, n, out, [&](uint32_t q) { return b + d[q].offset; },
+            [&](uint32_t q) { return d[q]; });
 
     int cur = 0;
     uint32_t i = 0;
@@ -279,7 +408,6 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
         while (i < n && k < c->max_desc) {
             const uint64_t o = d[i].offset;
             const uint64_t e = o + (d[i].len > 0 ? (uint64_t)d[i].len : 0);
-            if (e > base_bytes) return LVLIP_EINVAL;
             const uint64_t nlo = (o & ~15ull) < lo16 ? (o & ~15ull) : lo16;
             const uint64_t nhi = e > hi ? e : hi;
             if (align16(nhi) - nlo > c->arena) {
@@ -292,7 +420,13 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
             ++i;
         }
         const uint64_t span = hi > lo16 ? hi - lo16 : 0;
-        if (span) {
+        const uint8_t* from = nullptr;
+        if (span && reg) {
+            // f3 DMA: the copy engine reads the registered span directly.  Its
+            // last bytes up to the next 16 B may lie past base_bytes, so copy
+            // exactly `span` and let the kernel's 16-B tail read the arena.
+            from = b + lo16;
+        } else if (span) {
             uint8_t* dst = s.h_bytes;
             const uint8_t* src = b + lo16;
             parallel_ranges(c->threads, span, 4u << 20, [=](uint64_t lo, uint64_t hi) {
@@ -303,7 +437,7 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
             s.h_desc[q] = d[first + q];
             s.h_desc[q].offset = d[first + q].offset - lo16;
         }
-        rc = launch_piece(c, s, span ? span : 16, k, out + first);
+        rc = launch_piece(c, s, span ? span : 16, k, out + first, from);
         cur ^= 1;
     }
     for (auto& s : c->slot) {

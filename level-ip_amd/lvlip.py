@@ -29,6 +29,7 @@ LAB_PATH = os.path.join(HERE, "liblvlip_lab.so")
 # error codes (include/lvlip_csum.h)
 OK, EINVAL, ENODEV, EHIP, ENOMEM, ERANGE = 0, -1, -2, -3, -4, -5
 KERNEL_AUTO, KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_FLAT, KERNEL_WAVE_SIMPLE = 0, 1, 2, 3, 4
+REG_DMA, REG_ZEROCOPY = 0, 1
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "wave_lds": KERNEL_WAVE_LDS,
                 "flat": KERNEL_FLAT, "wave_simple": KERNEL_WAVE_SIMPLE, "flat_v1": 5}
 
@@ -128,6 +129,9 @@ SIGNATURES = {
     "lvlip_csum_batch_host_flat": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                                   ctypes.c_void_p, ctypes.c_uint32,
                                                   ctypes.c_void_p]),
+    "lvlip_csum_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_uint32]),
+    "lvlip_csum_unregister": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "lvlip_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     # include/lvlip_skb.h (f1/f2 frame batches)
     "lvlip_rx_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Frame), ctypes.c_uint32,
@@ -393,6 +397,18 @@ class Context:
                                                descs.ctypes.data, n, out.ctypes.data),
                "lvlip_csum_batch_host_flat")
         return out
+
+    def register(self, buf: np.ndarray, flags: int = REG_DMA) -> None:
+        """f3: pin `buf` (a contiguous uint8 array kept alive by the caller) in
+        place; batches inside it skip the pinned-arena gather."""
+        a = buf.view(np.uint8).reshape(-1)
+        if not a.flags.c_contiguous:
+            raise ValueError("register needs a contiguous buffer")
+        _check(_lib.lvlip_csum_register(self._h, a.ctypes.data, a.size, flags),
+               "lvlip_csum_register")
+
+    def unregister(self, buf: np.ndarray) -> None:
+        _check(_lib.lvlip_csum_unregister(self._h, buf.ctypes.data), "lvlip_csum_unregister")
 
     def rx_verify(self, frames, flags: int = 0) -> np.ndarray:
         """lvlip_rx_verify (f1): one verdict per frame (RX_*), frames untouched."""

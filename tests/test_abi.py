@@ -75,6 +75,8 @@ def test_error_paths_without_gpu():
     # n == 0 is a no-op success
     assert L.lvlip_csum_batch_dev(None, None, 0, None, None) == lvlip.OK
     assert L.lvlip_csum_ctx_destroy(None) == lvlip.EINVAL
+    assert L.lvlip_csum_register(None, 4096, 4096, 0) == lvlip.EINVAL
+    assert L.lvlip_csum_unregister(None, 4096) == lvlip.EINVAL
     assert L.lvlip_strerror(lvlip.ERANGE) == b"batch exceeds context arena"
     cfg = lvlip.LaunchCfg(99, 0, 0, 0)
     assert L.lvlip_csum_batch_dev_ex(16 * 1024, 16, 1, 16, None, ctypes.byref(cfg)) == lvlip.EINVAL

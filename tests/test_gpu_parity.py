@@ -282,3 +282,31 @@ def test_lab_read_probe_sums():
         assert rc == 0
         torch.cuda.synchronize()
         assert int(sink.item()) & 0xFFFFFFFF == int(h), (mode, unroll, nt)
+
+
+@pytest.mark.parametrize("flags", [lvlip.REG_DMA, lvlip.REG_ZEROCOPY])
+def test_host_registered_regions(flags):
+    """f3: registered host memory (DMA straight from it, or read in place by the
+    kernel over PCIe) gives the same bits as the gathered path."""
+    b = workloads.make("mixed", n=20000)
+    host = np.empty(b.nbytes + 4096 + 7, dtype=np.uint8)
+    buf = host[7:7 + b.nbytes]  # deliberately not 16-B aligned
+    buf[:] = b.host_bytes()
+    want = pyoracle.batch(buf, b.descs, threads=THREADS)
+    with lvlip.Context(0, arena_bytes=1 << 20) as ctx:
+        ctx.register(buf, flags)
+        assert np.array_equal(ctx.batch_host_flat(buf, b.descs), want)
+        # scattered packets inside the region (iov): zero-copy needs no gather
+        pk = [buf[int(d["offset"]):int(d["offset"]) + int(d["len"])] for d in b.descs[:5000]]
+        st = [int(d["start_sum"]) for d in b.descs[:5000]]
+        assert np.array_equal(ctx.batch_host(pk, st), want[:5000])
+        # a packet outside every region falls back to the gather, same bits
+        extra = np.frombuffer(b"\x01\x02\x03", dtype=np.uint8)
+        got = ctx.batch_host(pk[:10] + [extra], st[:10] + [0])
+        assert list(got[:10]) == list(want[:10])
+        assert int(got[10]) == pyoracle.checksum(extra, 3, 0)
+        with pytest.raises(lvlip.LvlipError):
+            ctx.register(buf[100:200], flags)  # overlaps
+        ctx.unregister(buf)
+        assert np.array_equal(ctx.batch_host_flat(buf, b.descs), want)
+        ctx.register(buf, flags)  # left registered: destroy releases it
