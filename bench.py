@@ -40,7 +40,10 @@ WORKLOAD_TEXT = {
                "16-B aligned slots (stride 9008)",
     "mixed": "2M frames: 20 B IPv4 headers + 64-1460 B ICMP/TCP payloads interleaved "
              "(4M descriptors, skb offsets 14/34)",
+    "tcp1500x64m": "64M x 1500 B TCP segments (96 GB) split over the ranks (strong scaling), "
+                   "16-B aligned slots (stride 1504)",
 }
+STRONG = {"tcp1500x64m": 64 << 20}  # workload -> total packets over all ranks
 
 
 def parse():
@@ -170,9 +173,16 @@ def main():
         raise SystemExit("bench.py needs a HIP device")
 
     kernel = lvlip.KERNEL_NAMES[args.kernel]
-    # weak scaling: each rank owns the next n packets of the stream
-    n = args.n or (1 << 21 if args.workload == "mixed" else 1 << 20)
-    b = workloads.make(args.workload, n=n, first=rank * n)
+    if args.workload in STRONG:
+        # strong scaling: a fixed batch, contiguous packet ranges per rank
+        total = args.n or STRONG[args.workload]
+        first = total * rank // world
+        n = total * (rank + 1) // world - first
+    else:
+        # weak scaling: each rank owns the next n packets of the stream
+        n = args.n or (1 << 21 if args.workload == "mixed" else 1 << 20)
+        first = rank * n
+    b = workloads.make(args.workload, n=n, first=first)
     base, descs, out = workloads.to_device(b, dev)
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
@@ -208,7 +218,7 @@ def main():
     wall_max, kern_ms_max = float(t[0]), float(t[1])
 
     total_bytes = b.algo_bytes * world  # equal shards (uniform), near-equal for mixed
-    if world > 1 and args.workload == "mixed":
+    if world > 1 and (args.workload == "mixed" or args.workload in STRONG):
         tb = torch.tensor([float(b.algo_bytes)], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tb)
         total_bytes = float(tb[0])
@@ -222,7 +232,7 @@ def main():
     diag = {}
     if rank == 0 and args.sweep:
         diag["sweep"] = sweep(lvlip, torch, base, descs, out, b, stream)
-    if rank == 0:
+    if rank == 0 and base.numel() < (1 << 34):
         diag["read_probe_GBps"] = read_probe(lvlip, torch, base, stream)
     if rank == 0 and args.e2e:
         diag["e2e_host_GBps"] = e2e(lvlip, b, base)
@@ -238,7 +248,8 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall_max * 1e3 / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+            "higher_is_better": True, "scaling": "strong" if args.workload in STRONG else "weak",
+            "vs_baseline": None, "dtype": "u16",
             "data": "synthetic (splitmix64 seed 0x1E7E1C5, 1% all-0x00 + 1% all-0xff packets), "
                     "device-resident",
             "config": {"workload": f"{args.workload}: {WORKLOAD_TEXT[args.workload]}",

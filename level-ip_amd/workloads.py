@@ -150,6 +150,8 @@ CONFIGS = {
     "tcp1500": lambda first=0, n=1 << 20: uniform(n, 1500, first, name="tcp1500"),
     "tcp9000": lambda first=0, n=1 << 20: uniform(n, 9000, first, name="tcp9000"),
     "mixed": lambda first=0, n=1 << 21: mixed(n, first),
+    # config #5: 64 M x 1500 B = 96 GB, fits one 288 GB MI355X; strong scaling
+    "tcp1500x64m": lambda first=0, n=64 << 20: uniform(n, 1500, first, name="tcp1500x64m"),
 }
 # layout variants of configs[1] for the lab scripts (slot stride: packed,
 # 128-B lines, 2 KiB NIC-style buffers); not bench workloads

@@ -220,6 +220,39 @@ def test_full_size_bit_exact(name):
     torch.cuda.empty_cache()
 
 
+def test_config5_96gb_chunked():
+    """BASELINE config #5 on one GPU: 64 M x 1500 B = 96 GB in HBM (offsets far
+    past 2^32).  Every output is compared with the oracle over the same bytes,
+    copied back 3 GB at a time; the flat kernel must agree with AUTO (stream)."""
+    n = 64 << 20
+    free, _ = torch.cuda.mem_get_info()
+    assert free > 110e9, f"config #5 needs ~98 GB of HBM, {free / 1e9:.0f} GB free"
+    b = workloads.make("tcp1500x64m")
+    assert b.n == n and b.nbytes > 96e9
+    base, descs, out = workloads.to_device(b)
+    lvlip.batch_torch(base, descs, out, len_hint=1500)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint16).copy()
+    out2 = torch.empty_like(out)
+    lvlip.batch_torch(base, descs, out2, kernel=lvlip.KERNEL_FLAT)
+    torch.cuda.synchronize()
+    assert np.array_equal(out2.cpu().numpy().view(np.uint16), got)
+    del out2
+    step = 2 << 20
+    for lo in range(0, n, step):
+        hi = min(n, lo + step)
+        d = b.descs[lo:hi].copy()
+        start = int(d["offset"][0])
+        stop = (int(d["offset"][-1]) + int(d["len"][-1]) + 15) & ~15
+        host = base[start:stop].cpu().numpy()
+        d["offset"] -= np.uint64(start)
+        want = pyoracle.batch(host, d, threads=THREADS)
+        bad = np.nonzero(got[lo:hi] != want)[0]
+        assert bad.size == 0, f"chunk {lo}: {bad.size} differ, first {bad[:5] + lo}"
+    del base, descs, out
+    torch.cuda.empty_cache()
+
+
 def test_empty_and_tiny_batches():
     base = torch.zeros(64, dtype=torch.uint8, device="cuda")
     descs = dev_descs(mk_descs([0], [0], [0]))
