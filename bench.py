@@ -236,6 +236,7 @@ def main():
         diag["read_probe_GBps"] = read_probe(lvlip, torch, base, stream)
     if rank == 0 and args.e2e:
         diag["e2e_host_GBps"] = e2e(lvlip, b, base)
+        diag["latency_us"] = latency(lvlip, torch, dev)
 
     cpu, verified = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -317,6 +318,41 @@ def read_probe(lvlip, torch, base, stream):
         best[f"m{mode}u{u}nt{nt}b{bpc}"] = round(nb / ms / 1e6, 1)
     log("read_probe GB/s", best)
     return best
+
+
+def latency(lvlip, torch, dev):
+    """Small-batch latency (diagnostic): one call's wall time for n x 1500 B,
+    device-resident (launch + kernel, synchronised) and host-resident (gather +
+    H2D + kernel + D2H).  Where a CPU per-call loop wins is read off these."""
+    import workloads
+
+    res = {}
+    for n in (64, 1024, 16384):
+        b = workloads.make("tcp1500", n=n)
+        base, descs, out = workloads.to_device(b, dev)
+        stream = torch.cuda.current_stream(dev)
+
+        def f():
+            lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(), stream.cuda_stream,
+                            lvlip.KERNEL_AUTO, 0, 0, 1500)
+            stream.synchronize()
+
+        for _ in range(20):
+            f()
+        t0 = time.perf_counter()
+        for _ in range(200):
+            f()
+        res[f"dev_n{n}_us"] = round((time.perf_counter() - t0) / 200 * 1e6, 1)
+        host = b.host_bytes()
+        with lvlip.Context(dev.index or 0, arena_bytes=64 << 20) as ctx:
+            for _ in range(20):
+                ctx.batch_host_flat(host, b.descs)
+            t0 = time.perf_counter()
+            for _ in range(100):
+                ctx.batch_host_flat(host, b.descs)
+            res[f"host_n{n}_us"] = round((time.perf_counter() - t0) / 100 * 1e6, 1)
+    log("latency us", res)
+    return res
 
 
 def e2e(lvlip, b, base):

@@ -343,3 +343,51 @@ def test_host_registered_regions(flags):
         ctx.unregister(buf)
         assert np.array_equal(ctx.batch_host_flat(buf, b.descs), want)
         ctx.register(buf, flags)  # left registered: destroy releases it
+
+
+def test_contexts_in_threads():
+    """One context per thread (the reference checksums from the core, IPC and
+    timer threads, src/main.c:83-89): concurrent host batches stay bit-exact."""
+    import threading
+
+    b = workloads.make("mixed", n=8000)
+    host = b.host_bytes()
+    want = pyoracle.batch(host, b.descs, threads=THREADS)
+    errors = []
+
+    def worker(k):
+        try:
+            with lvlip.Context(0, arena_bytes=(256 << 10) * (k + 1)) as ctx:
+                for _ in range(3):
+                    if not np.array_equal(ctx.batch_host_flat(host, b.descs), want):
+                        errors.append(f"thread {k}: mismatch")
+        except Exception as e:  # pragma: no cover
+            errors.append(f"thread {k}: {e}")
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+
+
+def test_batch_dev_on_user_stream_and_graph():
+    """batch_dev is asynchronous on the caller's stream and capturable in a HIP
+    graph (the replay recomputes into the same output)."""
+    b = workloads.make("tcp1500", n=4096)
+    base, descs, out = workloads.to_device(b)
+    want = pyoracle.batch(base.cpu().numpy(), b.descs, threads=THREADS)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        lvlip.batch_torch(base, descs, out, stream=s, len_hint=1500)
+    s.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    out.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        lvlip.batch_torch(base, descs, out, stream=torch.cuda.current_stream(), len_hint=1500)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
