@@ -9,24 +9,28 @@
  * (called concurrently from the core, IPC and timer threads).
  *
  * Bit-exactness: the reference adds u16 words into a uint32_t with plain
- * wrap-around.  Accumulating the same words in 64 bits and truncating once is
- * the same value mod 2^32, so the result is identical for every count.
+ * wrap-around.  Any grouping of the same words summed mod 2^32 is the same
+ * value, so the wider accumulations below (packed 64-bit fields; AVX2 u32
+ * lanes, picked at run time when the CPU has it) give identical results for
+ * every count and alignment.  LVLIP_CPU_SCALAR=1 forces the portable loop.
  */
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 #include "lvlip_csum.h"
 
-/* src/utils.c:22-38 */
-uint32_t sum_every_16bits(void *addr, int count)
+/* Portable word sum: 16 bytes per step, eight native-endian u16 words into two
+ * accumulators of two 32-bit fields each.  A field gains <= 2 * 0xffff per
+ * step, so 16384 steps stay below 2^31 and no field carries into its
+ * neighbour. */
+static uint32_t sum_words_scalar(const uint8_t *p, int count)
 {
-    const uint8_t *p = (const uint8_t *)addr;
     uint64_t s0 = 0, s1 = 0;
-
-    /* 16 bytes per step: eight native-endian u16 words into two accumulators
-     * of two 32-bit fields each.  A field gains <= 2 * 0xffff per step, so
-     * 16384 steps stay below 2^31 and no field carries into its neighbour. */
     while (count >= 16) {
         int steps = count >> 4;
         if (steps > 16384)
@@ -54,6 +58,60 @@ uint32_t sum_every_16bits(void *addr, int count)
     if (count > 0) /* utils.c:34-35: left-over byte, zero-extended */
         s0 += *p;
     return (uint32_t)(s0 + s1);
+}
+
+#if defined(__x86_64__)
+/* AVX2: 64 bytes per step, each u16 word widened to a u32 lane.  Lanes wrap
+ * mod 2^32, which is exactly the reference's arithmetic, so no flushing. */
+__attribute__((target("avx2"))) static uint32_t sum_words_avx2(const uint8_t *p, int count)
+{
+    const __m256i z = _mm256_setzero_si256();
+    __m256i a0 = z, a1 = z, a2 = z, a3 = z;
+    while (count >= 64) {
+        const __m256i v0 = _mm256_loadu_si256((const __m256i *)(const void *)p);
+        const __m256i v1 = _mm256_loadu_si256((const __m256i *)(const void *)(p + 32));
+        a0 = _mm256_add_epi32(a0, _mm256_unpacklo_epi16(v0, z));
+        a1 = _mm256_add_epi32(a1, _mm256_unpackhi_epi16(v0, z));
+        a2 = _mm256_add_epi32(a2, _mm256_unpacklo_epi16(v1, z));
+        a3 = _mm256_add_epi32(a3, _mm256_unpackhi_epi16(v1, z));
+        p += 64;
+        count -= 64;
+    }
+    const __m256i a = _mm256_add_epi32(_mm256_add_epi32(a0, a1), _mm256_add_epi32(a2, a3));
+    uint32_t lanes[8];
+    _mm256_storeu_si256((__m256i *)(void *)lanes, a);
+    uint32_t s = 0;
+    for (int i = 0; i < 8; i++)
+        s += lanes[i];
+    return s + sum_words_scalar(p, count);
+}
+#endif
+
+typedef uint32_t (*sum_fn)(const uint8_t *, int);
+static sum_fn g_sum; /* chosen once; racing first callers store the same value */
+
+static sum_fn pick_sum(void)
+{
+    sum_fn f = sum_words_scalar;
+#if defined(__x86_64__)
+    const char *force = getenv("LVLIP_CPU_SCALAR");
+    __builtin_cpu_init();
+    if (!(force && force[0] == '1') && __builtin_cpu_supports("avx2"))
+        f = sum_words_avx2;
+#endif
+    __atomic_store_n(&g_sum, f, __ATOMIC_RELAXED);
+    return f;
+}
+
+/* src/utils.c:22-38 */
+uint32_t sum_every_16bits(void *addr, int count)
+{
+    if (count <= 0)
+        return 0;
+    sum_fn f = __atomic_load_n(&g_sum, __ATOMIC_RELAXED);
+    if (!f)
+        f = pick_sum();
+    return f((const uint8_t *)addr, count);
 }
 
 /* src/utils.c:40-55 */

@@ -114,18 +114,20 @@ def pseudo_sum(saddr: int, daddr: int, proto: int, length: int) -> int:
 
 
 def batch(base: np.ndarray, descs: np.ndarray, threads: int = 1, opt: int = 2,
-          use_reference: bool = False) -> np.ndarray:
+          use_reference: bool = False, csum_fn=None) -> np.ndarray:
     """out[i] = checksum(base + off_i, len_i, start_i) on the CPU.
 
     use_reference=True calls the reference's own checksum() from oracle/_ref per
-    packet (pthreads over contiguous packet ranges)."""
+    packet (pthreads over contiguous packet ranges); csum_fn (a ctypes function
+    with checksum()'s signature) times another per-call implementation with the
+    same harness (bench.py's diag of the product's CPU drop-in)."""
     base = _u8(base)
     descs = np.ascontiguousarray(descs)
     assert descs.dtype.itemsize == 16
     n = descs.size
     out = np.empty(n, dtype=np.uint16)
     lib = liblib(opt)
-    fn = None
+    fn = ctypes.cast(csum_fn, ctypes.c_void_p) if csum_fn is not None else None
     if use_reference:
         ref = reflib()
         if ref is None:

@@ -136,3 +136,44 @@ def test_ip_send_check_symbol_matches_reference():
             ref.ip_send_check(ctypes.addressof(c))
             del c
             assert a == b
+
+
+def _word_sum(a: np.ndarray, ln: int) -> int:
+    w = int(a[: ln & ~1].view("<u2").astype(np.uint64).sum())
+    if ln & 1:
+        w += int(a[ln - 1])
+    return w & 0xFFFFFFFF
+
+
+def test_sum_every_alignment_and_length():
+    """Every alignment 0-63 x lengths 0-300 and the config sizes (the SIMD loop,
+    its scalar tail and the portable loop all see their edges)."""
+    rng = np.random.default_rng(17)
+    buf = rng.integers(0, 256, 1 << 15, dtype=np.uint8)
+    for off in range(64):
+        for ln in list(range(0, 301)) + [1499, 1500, 1501, 9000, 9001]:
+            a = buf[off:off + ln]
+            assert lvlip.sum_every_16bits(a if ln else b"\0", ln) == _word_sum(a, ln), (off, ln)
+
+
+def test_portable_loop_forced():
+    """LVLIP_CPU_SCALAR=1 selects the portable loop; same results (subprocess:
+    the choice is made once per process)."""
+    import os
+    import subprocess
+    import sys
+
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import numpy as np, lvlip\n"
+        "rng = np.random.default_rng(5); b = rng.integers(0, 256, 300000, dtype=np.uint8)\n"
+        "for off in range(17):\n"
+        "  for ln in (0, 1, 15, 16, 17, 63, 64, 65, 1500, 262145, 299000):\n"
+        "    a = b[off:off + ln]\n"
+        "    w = int(a[: ln & ~1].view('<u2').astype(np.uint64).sum()) + (int(a[-1]) if ln & 1 else 0)\n"
+        "    assert lvlip.sum_every_16bits(a if ln else b'\\0', ln) == w & 0xFFFFFFFF, (off, ln)\n"
+        "print('ok')\n" % os.path.dirname(lvlip.__file__))
+    env = dict(os.environ, LVLIP_CPU_SCALAR="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr
