@@ -60,6 +60,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--sweep", action="store_true", help="also time every kernel variant (stderr)")
+    p.add_argument("--origin", choices=["local", "root"], default="local",
+                   help="root: the whole batch starts on rank 0's GPU and is scattered "
+                        "point to point first (timed separately, diag.scatter)")
     p.add_argument("--e2e", action="store_true",
                    help="also time the host-resident path (PCIe-inclusive; stderr + diag)")
     return p.parse_args()
@@ -190,8 +193,41 @@ def main():
         # weak scaling: each rank owns the next n packets of the stream
         n = args.n or (1 << 21 if args.workload == "mixed" else 1 << 20)
         first = rank * n
-    b = workloads.make(args.workload, n=n, first=first)
-    base, descs, out = workloads.to_device(b, dev)
+    scatter_diag = None
+    if args.origin == "root" and world > 1:
+        import shard
+
+        # the batch originates on one GPU; each rank receives its
+        # byte-balanced shard point to point (RCCL over xGMI), timed on its own
+        total_n = n * world if args.workload not in STRONG else (args.n or STRONG[args.workload])
+        full, fdescs = None, None
+        if rank == 0:
+            fb = workloads.make(args.workload, n=total_n, first=0)
+            fbase, _, _ = workloads.to_device(fb, dev)
+            full = fbase if backend == "nccl" else fbase.cpu()
+            fdescs = fb.descs
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        ts = time.perf_counter()
+        local, ldescs, _ = shard.scatter_from_root(full, fdescs, coll_dev)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t_sc = time.perf_counter() - ts
+        sent = torch.tensor([float(local.numel())], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(sent)
+        scatter_diag = {"seconds": round(t_sc, 4), "bytes": int(sent[0]),
+                        "GBps": round(float(sent[0]) / t_sc / 1e9, 2)}
+        b = workloads.Batch(args.workload, ldescs, int(local.numel()),
+                            np.zeros(ldescs.size, np.uint8), 0,
+                            int(np.maximum(ldescs["len"], 0).sum()))
+        base = torch.zeros((local.numel() + 15) // 16 * 16 + 16, dtype=torch.uint8, device=dev)
+        base[: local.numel()] = local.to(dev)
+        descs = torch.from_numpy(ldescs.view(np.uint8).copy()).to(dev)
+        out = torch.empty(max(b.n, 1), dtype=torch.int16, device=dev)
+        del full, local
+    else:
+        b = workloads.make(args.workload, n=n, first=first)
+        base, descs, out = workloads.to_device(b, dev)
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
 
@@ -226,7 +262,7 @@ def main():
     wall_max, kern_ms_max = float(t[0]), float(t[1])
 
     total_bytes = b.algo_bytes * world  # equal shards (uniform), near-equal for mixed
-    if world > 1 and (args.workload == "mixed" or args.workload in STRONG):
+    if world > 1 and (args.workload == "mixed" or args.workload in STRONG or args.origin == "root"):
         tb = torch.tensor([float(b.algo_bytes)], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tb)
         total_bytes = float(tb[0])
@@ -238,6 +274,8 @@ def main():
         if kernel == lvlip.KERNEL_AUTO else args.kernel)
 
     diag = {}
+    if scatter_diag is not None:
+        diag["scatter"] = scatter_diag
     if rank == 0 and args.sweep:
         diag["sweep"] = sweep(lvlip, torch, base, descs, out, b, stream)
     if rank == 0 and base.numel() < (1 << 34):

@@ -7,9 +7,13 @@ descriptor ranges with no exchange on the data path:
                            a ragged batch gives every rank about the same HBM
                            traffic, which is what bounds the kernel
   local_batch(...)         a rank's descriptors rebased to its own byte span
+  scatter_from_root(...)   when the batch originates on one GPU: each rank's
+                           bytes and descriptors sent point to point from the
+                           root (RCCL over xGMI), timed separately from the
+                           kernel
   gather_results(...)      results back in batch order (torch.distributed
-                           all_gather: RCCL on GPUs, gloo on CPU tests), the only
-                           collective, 2 bytes per packet
+                           all_gather: RCCL on GPUs, gloo on CPU tests), 2 bytes
+                           per packet
 
 bench.py's weak-scaling run does not move packets at all: each rank
 generates its own shard of the stream (workloads.make(first=rank*n)).
@@ -72,3 +76,51 @@ def gather_results(local_out, counts: list[int], group=None):
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
     return torch.cat([p[:c] for p, c in zip(parts, counts)]).to(torch.int16)
+
+
+def scatter_from_root(buf, descs, device, group=None, root: int = 0):
+    """Distribute a batch held by `root` (buf: uint8 tensor, descs: DESC_DTYPE
+    array; both ignored on other ranks).  Returns this rank's
+    (local_buf uint8 tensor on `device`, local_descs array, (lo, hi)).
+
+    The partition is byte-balanced and contiguous (partition()); each rank's
+    byte span travels as one send from the root, so the only traffic is the
+    data itself plus 16 B per descriptor."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    meta = torch.zeros((world, 4), dtype=torch.int64, device=device)  # lo, hi, start, span
+    plan = []
+    if rank == root:
+        for lo, hi in partition(descs["len"], world):
+            d, start, span = local_batch(descs, lo, hi)
+            plan.append((d, start, span))
+            meta[len(plan) - 1] = torch.tensor([lo, hi, start, span], dtype=torch.int64)
+    dist.broadcast(meta, src=root, group=group)
+    m = meta.cpu().tolist()
+    if rank == root:
+        reqs = []
+        for r in range(world):
+            if r == root:
+                continue
+            d, start, span = plan[r]
+            if m[r][1] > m[r][0]:
+                dt = torch.from_numpy(d.view(np.uint8).copy()).to(device)
+                reqs.append(dist.isend(dt, dst=r, group=group))
+            if span:
+                reqs.append(dist.isend(buf[start:start + span].contiguous(), dst=r, group=group))
+        for q in reqs:
+            q.wait()
+        d, start, span = plan[root]
+        return buf[start:start + span].clone(), d, (m[root][0], m[root][1])
+    lo, hi, start, span = m[rank]
+    d = np.zeros(hi - lo, dtype=DESC_DTYPE)
+    if hi > lo:
+        dt = torch.empty((hi - lo) * DESC_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        dist.recv(dt, src=root, group=group)
+        d = dt.cpu().numpy().view(DESC_DTYPE).copy()
+    local = torch.empty(span, dtype=torch.uint8, device=device)
+    if span:
+        dist.recv(local, src=root, group=group)
+    return local, d, (lo, hi)

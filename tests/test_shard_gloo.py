@@ -86,3 +86,56 @@ def test_two_rank_gloo_shards_match_single_batch():
         p.join(170)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+def _scatter_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, "..", "level-ip_amd"), os.path.join(here, "..", "oracle")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+
+    import pyoracle
+    import shard as sh
+    import workloads as wl
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        buf, descs = None, None
+        if rank == 0:  # the batch originates on one rank only
+            b = wl.make("mixed", n=2500)
+            buf, descs = torch.from_numpy(b.host_bytes()), b.descs
+        local, d, (lo, hi) = sh.scatter_from_root(buf, descs, torch.device("cpu"))
+        out = pyoracle.batch(local.numpy(), d) if d.size else np.zeros(0, np.uint16)
+        counts = [0] * world
+        cnt = torch.tensor([hi - lo], dtype=torch.int64)
+        allc = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allc, cnt)
+        counts = [int(c) for c in allc]
+        res = sh.gather_results(torch.from_numpy(out.view(np.int16).copy()), counts)
+        if rank == 0:
+            full = pyoracle.batch(buf.numpy(), descs)
+            q.put(bool(np.array_equal(res.numpy().view(np.uint16), full)) and sum(counts) == descs.size)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [2, 3])
+def test_scatter_from_root_then_gather(world):
+    """Batch held by rank 0 only: scatter byte-balanced shards point to point,
+    checksum each shard, all-gather: equals the single batch bit for bit."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(170)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
