@@ -35,6 +35,7 @@
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
@@ -222,6 +223,9 @@ __global__ __launch_bounds__(256) void k_wave_simple(const uint8_t* __restrict__
 constexpr int SW_WAVES = 4;  // waves per 256-thread workgroup
 constexpr uint32_t SRD_WORD3 = 0x00020000u;  // raw 32-bit buffer, as make_buffer_rsrc
 
+// POL (A/B knob): 0 nt (default), 1 default policy, 2 nt sc1,
+// 3 nt sc0 sc1, 4 sc1
+template <int POL = 0>
 __device__ __forceinline__ u32x4 buffer_load_nt_asm(uint32_t voff, const u32x4 srd) {
     // The resource must sit in SGPRs; it is wave-uniform by construction, which
     // readfirstlane makes explicit to the compiler (cdna_hip_programming.md T20).
@@ -234,9 +238,26 @@ __device__ __forceinline__ u32x4 buffer_load_nt_asm(uint32_t voff, const u32x4 s
     // (a VALU write of SGPRs); a VMEM read of such SGPRs needs 5 wait states on
     // gfx9-family parts, and hipcc inserts no hazard padding around inline asm.
     u32x4 r;
-    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen nt"
-                 : "=v"(r)
-                 : "v"(voff), "s"(s));
+    if (POL == 0)
+        asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen nt"
+                     : "=v"(r)
+                     : "v"(voff), "s"(s));
+    else if (POL == 1)
+        asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen"
+                     : "=v"(r)
+                     : "v"(voff), "s"(s));
+    else if (POL == 2)
+        asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen nt sc1"
+                     : "=v"(r)
+                     : "v"(voff), "s"(s));
+    else if (POL == 3)
+        asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen sc0 sc1 nt"
+                     : "=v"(r)
+                     : "v"(voff), "s"(s));
+    else
+        asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen sc1"
+                     : "=v"(r)
+                     : "v"(voff), "s"(s));
     return r;
 }
 
@@ -315,7 +336,7 @@ __device__ __forceinline__ void piece_wait(u32x4& a, u32x4& b) {
 // piece.  R pieces are in flight; the oldest is retired by vmcnt(2*(R-1)).
 // (r01 profile of a per-1KiB-slot ring: ~130 SALU per packet, the CU's scalar
 // unit ~80 % busy and the kernel SALU-bound; this layout cuts that ~3x.)
-template <int R>
+template <int R, int POL = 0>
 __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base,
                                                 const lvlip_csum_desc* __restrict__ descs,
                                                 uint32_t n, uint32_t per_wave,
@@ -382,8 +403,8 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
         u32x4 sr = srd;
         if (!live) sr.z = 0;  // past the range: every dword out of range -> zeros
         const uint32_t off = lane16 + io;
-        va[r] = buffer_load_nt_asm(off, sr);
-        vb[r] = buffer_load_nt_asm(off + 1024u, sr);
+        va[r] = buffer_load_nt_asm<POL>(off, sr);
+        vb[r] = buffer_load_nt_asm<POL>(off + 1024u, sr);
         // srd.z = round_up(len, 4): the piece is the packet's last when it reaches
         // that (or the packet is empty)
         const bool last = io + PIECE >= srd.z;
@@ -738,7 +759,7 @@ __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
     return ((1u << w) - 1u) << (8 * s);
 }
 
-template <int U>
+template <int U, bool NT = true, bool CONTIG = true>
 __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
                                               const lvlip_csum_desc* __restrict__ descs,
                                               uint32_t n, uint16_t* __restrict__ out) {
@@ -820,8 +841,18 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
     // val - P, the lane holding its last chunk (or lane 63) adds P, and a
     // segment that starts at lane 0 as a continuation needs nothing (exclusive
     // prefix 0).  One LDS atomic per group carries both.
+    //
+    // Group order: wave w takes groups [w*G/4, (w+1)*G/4) in rounds of U
+    // consecutive groups (CONTIG), so the 128-B line two neighbouring groups
+    // share is requested twice back to back by one wave, and merges in L2,
+    // instead of by two waves at different times (PMC: 4.4 % re-fetched lines
+    // with the interleaved order).
+    const uint32_t gstep = CONTIG ? 1u : 4u;
+    const uint32_t gper = (G + 3u) / 4u;
+    const uint32_t g_lo = CONTIG ? wid * gper : wid;
+    const uint32_t g_end = CONTIG ? (g_lo + gper < G ? g_lo + gper : G) : G;
     if (C > 0) {
-        for (uint32_t gr = wid; gr < G; gr += 4u * U) {
+        for (uint32_t gr = g_lo; gr < g_end; gr += gstep * U) {
             uint4 x[U];
             uint32_t mt[U], kk[U];
             bool vl[U];
@@ -829,8 +860,8 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
             bool gv[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t g = gr + 4u * u;
-                gv[u] = g < G;
+                const uint32_t g = gr + gstep * u;
+                gv[u] = g < g_end;
                 const uint32_t gc = gv[u] ? g : G - 1u;
                 const uint2 gg = s_grp[gc];
                 hlo[u] = uniform(gg.x);
@@ -853,10 +884,11 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
             for (int u = 0; u < U; ++u) rec[u] = s_rec[r[u]];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t j = (gr + 4u * u) * 64u + lane;
+                const uint32_t j = (gr + gstep * u) * 64u + lane;
                 vl[u] = gv[u] && j < C;
                 kk[u] = vl[u] ? j - rec[u].z : 0u;
-                x[u] = load_nt_global((((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * kk[u]);
+                const uint64_t ca = (((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * kk[u];
+                x[u] = NT ? load_nt_global(ca) : load_global(ca);
                 mt[u] = rec[u].w;
             }
 #pragma unroll
@@ -987,6 +1019,33 @@ void launch_wave_simple(uint32_t grid, hipStream_t s, const void* base, const lv
 
 // Persistent streaming launch: waves_per_cu waves on every CU, each owning a
 // contiguous range of ceil(n / waves) packets.
+// LVLIP_LOAD_POLICY (A/B knob, read once): the data loads' cache
+// policy.  nt (default) | temporal | nt_sc1 | nt_sc0sc1 | sc1; the flat kernel
+// knows nt and temporal only (anything else is nt there).
+int load_policy() {
+    static const int pol = [] {
+        const char* e = getenv("LVLIP_LOAD_POLICY");
+        if (!e) return 0;
+        if (!strcmp(e, "temporal")) return 1;
+        if (!strcmp(e, "nt_sc1")) return 2;
+        if (!strcmp(e, "nt_sc0sc1")) return 3;
+        if (!strcmp(e, "sc1")) return 4;
+        return 0;
+    }();
+    return pol;
+}
+bool load_nt() { return load_policy() != 1; }
+
+// LVLIP_FLAT_GROUPS=interleaved (A/B knob): k_flat2's waves take groups
+// w, w+4, ... instead of contiguous quarters of the tile.
+bool flat_contig() {
+    static const bool c = [] {
+        const char* e = getenv("LVLIP_FLAT_GROUPS");
+        return !(e && strcmp(e, "interleaved") == 0);
+    }();
+    return c;
+}
+
 template <int U>
 void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
                    uint32_t n, uint16_t* out) {
@@ -997,8 +1056,21 @@ void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvli
     waves = (waves + 3) & ~3ull;  // whole 256-thread blocks
     const uint32_t per_wave = (uint32_t)(((uint64_t)n + waves - 1) / waves);
     const uint32_t grid = (uint32_t)(waves / 4);
-    hipLaunchKernelGGL(lvlip::k_stream<U>, dim3(grid), dim3(256), 0, s,
-                       (const uint8_t*)base, d, n, per_wave, out);
+    switch (load_policy()) {
+#define LVLIP_STREAM_POL(P)                                                              \
+    case P:                                                                              \
+        hipLaunchKernelGGL((lvlip::k_stream<U, P>), dim3(grid), dim3(256), 0, s,         \
+                           (const uint8_t*)base, d, n, per_wave, out);                   \
+        break;
+        LVLIP_STREAM_POL(1)
+        LVLIP_STREAM_POL(2)
+        LVLIP_STREAM_POL(3)
+        LVLIP_STREAM_POL(4)
+#undef LVLIP_STREAM_POL
+        default:
+            hipLaunchKernelGGL((lvlip::k_stream<U, 0>), dim3(grid), dim3(256), 0, s,
+                               (const uint8_t*)base, d, n, per_wave, out);
+    }
 }
 
 template <int U>
@@ -1094,13 +1166,21 @@ int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint
         case LVLIP_KERNEL_FLAT: {
             const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
             if (unroll <= 0) unroll = 4;
-            switch (unroll) {
-                case 2: hipLaunchKernelGGL(lvlip::k_flat2<2>, dim3(grid), dim3(lvlip::FT), 0, s,
-                                           (const uint8_t*)base, descs, n, out); break;
-                case 4: hipLaunchKernelGGL(lvlip::k_flat2<4>, dim3(grid), dim3(lvlip::FT), 0, s,
-                                           (const uint8_t*)base, descs, n, out); break;
-                case 8: hipLaunchKernelGGL(lvlip::k_flat2<8>, dim3(grid), dim3(lvlip::FT), 0, s,
-                                           (const uint8_t*)base, descs, n, out); break;
+            const bool nt = load_nt();
+            const bool contig = flat_contig();
+            switch (unroll * 4 + (nt ? 2 : 0) + (contig ? 1 : 0)) {
+#define LVLIP_FLAT(UU, NTV, CG)                                                               \
+    case UU * 4 + (NTV ? 2 : 0) + (CG ? 1 : 0):                                              \
+        hipLaunchKernelGGL((lvlip::k_flat2<UU, NTV, CG>), dim3(grid), dim3(lvlip::FT), 0, s,  \
+                           (const uint8_t*)base, descs, n, out);                             \
+        break;
+                LVLIP_FLAT(2, true, true) LVLIP_FLAT(2, true, false)
+                LVLIP_FLAT(2, false, true) LVLIP_FLAT(2, false, false)
+                LVLIP_FLAT(4, true, true) LVLIP_FLAT(4, true, false)
+                LVLIP_FLAT(4, false, true) LVLIP_FLAT(4, false, false)
+                LVLIP_FLAT(8, true, true) LVLIP_FLAT(8, true, false)
+                LVLIP_FLAT(8, false, true) LVLIP_FLAT(8, false, false)
+#undef LVLIP_FLAT
                 default: return LVLIP_EINVAL;
             }
             break;

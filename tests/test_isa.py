@@ -66,7 +66,7 @@ def test_buffer_loads_padded_against_valu_sgpr_hazard(asm):
     for name, body in stream_kernels(asm).items():
         n = 0
         for i, ins in enumerate(body):
-            if ins.startswith("buffer_load_dwordx4") and ins.endswith("offen nt"):
+            if ins.startswith("buffer_load_dwordx4") and " offen" in ins:
                 n += 1
                 assert body[i - 1] == "s_nop 4", (name, i, body[i - 3:i + 1])
         assert n >= 2, name
