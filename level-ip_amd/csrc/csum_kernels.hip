@@ -174,8 +174,9 @@ __global__ __launch_bounds__(256) void k_wave_simple(const uint8_t* __restrict__
                                               uint32_t n, uint16_t* __restrict__ out) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wpb = blockDim.x >> 6;
-    const uint32_t stride = gridDim.x * wpb;
-    for (uint32_t p = uniform(blockIdx.x * wpb + (threadIdx.x >> 6)); p < n; p += stride) {
+    const uint64_t stride = (uint64_t)gridDim.x * wpb;
+    // 64-bit cursor: with n near LVLIP_MAX_BATCH a u32 p + stride would wrap
+    for (uint64_t p = uniform(blockIdx.x * wpb + (threadIdx.x >> 6)); p < n; p += stride) {
         const lvlip_csum_desc d = descs[p];
         uint32_t w = 0;
         if (d.len > 0) {
@@ -541,8 +542,8 @@ __global__ __launch_bounds__(256) void k_wave_lds(const uint8_t* __restrict__ ba
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wid = uniform(threadIdx.x >> 6);
     uint4* slab = slabs + wid * (U * 64);
-    const uint32_t stride = gridDim.x * 4u;
-    for (uint32_t p = uniform(blockIdx.x * 4u + wid); p < n; p += stride) {
+    const uint64_t stride = (uint64_t)gridDim.x * 4u;
+    for (uint64_t p = uniform(blockIdx.x * 4u + wid); p < n; p += stride) {
         const lvlip_csum_desc d = descs[p];
         uint32_t w = 0;
         if (d.len > 0) {
@@ -1106,12 +1107,13 @@ int lvlip_device_count(void) {
     return c;
 }
 
-int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint32_t n,
-                            uint16_t* out, void* stream, const lvlip_launch_cfg* cfg) {
-    if (n == 0) return LVLIP_OK;
-    if (!base || !descs || !out || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
-    if (((uintptr_t)base & 15u) != 0) return LVLIP_EINVAL;
-    hipStream_t s = (hipStream_t)stream;
+}  // extern "C"
+
+namespace {
+
+// One launch of the selected kernel over n <= kLaunchMax descriptors.
+int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uint16_t* out,
+                 hipStream_t s, const lvlip_launch_cfg* cfg) {
     int kernel = cfg ? cfg->kernel : LVLIP_KERNEL_AUTO;
     int unroll = cfg ? cfg->unroll : 0;
     int wpc = cfg ? cfg->waves_per_cu : 0;
@@ -1195,6 +1197,30 @@ int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    return LVLIP_OK;
+}
+
+// A dispatch's grid is at most 2^32 - 1 work-items on this runtime, and the
+// flat kernel runs one thread per descriptor: batches beyond kLaunchMax
+// descriptors go out as several launches on the same stream (offsets stay
+// relative to the same base, so nothing else changes).
+constexpr uint32_t kLaunchMax = 1u << 30;
+
+}  // namespace
+
+extern "C" {
+
+int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint32_t n,
+                            uint16_t* out, void* stream, const lvlip_launch_cfg* cfg) {
+    if (n == 0) return LVLIP_OK;
+    if (!base || !descs || !out || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
+    if (((uintptr_t)base & 15u) != 0) return LVLIP_EINVAL;
+    for (uint32_t lo = 0; lo < n;) {
+        const uint32_t m = n - lo < kLaunchMax ? n - lo : kLaunchMax;
+        const int rc = dispatch_one(base, descs + lo, m, out + lo, (hipStream_t)stream, cfg);
+        if (rc != LVLIP_OK) return rc;
+        lo += m;
+    }
     return LVLIP_OK;
 }
 

@@ -391,3 +391,73 @@ def test_batch_dev_on_user_stream_and_graph():
     g.replay()
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+
+
+def test_max_int_packet():
+    """The reference's `int count` at its maximum: one packet of INT_MAX bytes
+    (odd length, odd offset, u32 word sum wrapping ~16 times), plus a 1 GiB
+    all-0xff packet, through AUTO with and without the hint and every kernel."""
+    n1 = 2**31 - 1
+    base = torch.empty(n1 + 64 + (1 << 30) + 64, dtype=torch.uint8, device="cuda")
+    tk = lvlip.testkit()
+    assert tk.lvlip_testkit_fill(base.data_ptr(), base.numel() & ~7, 99, 0,
+                                 torch.cuda.current_stream().cuda_stream) == 0
+    off2 = (n1 + 64 + 15) & ~15
+    base[off2:off2 + (1 << 30)] = 0xFF
+    d = mk_descs([1, off2], [n1, 1 << 30], [0xFFFFFFFF, 0x12345678])
+    host = base.cpu().numpy()
+    want = pyoracle.batch(host, d, threads=2)
+    # 0xffff x 2^29 words = 0x1fffe0000000 -> wraps; fold of the seed + it
+    assert want[1] == pyoracle.checksum(np.full(16, 0xFF, np.uint8), 0, (0x12345678 + (0xFFFF << 29)) & 0xFFFFFFFF)
+    descs = dev_descs(d)
+    for variant in [(lvlip.KERNEL_AUTO, 0, 0), (lvlip.KERNEL_WAVE, 2, 0), (lvlip.KERNEL_FLAT, 0, 0),
+                    (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0)]:
+        assert list(run(base, descs, variant)) == list(want), variant
+    del base, descs
+    torch.cuda.empty_cache()
+
+
+def test_max_batch_descriptor_count():
+    """n = LVLIP_MAX_BATCH (0xFFFFFFF0, ~4.3 G descriptors, 68.7 GB of
+    descriptors in HBM): index arithmetic past 2^31 in every launch path.
+    Packets repeat with period 7168 (offset (i % 1024) * 16 + i % 3, length
+    20 + i % 7), so all outputs are checked on the GPU against 7168 oracle
+    values."""
+    n = 0xFFFFFFF0
+    free, _ = torch.cuda.mem_get_info()
+    assert free > 90e9, f"needs ~80 GB of HBM, {free / 1e9:.0f} GB free"
+    period = 7168
+    rng = np.random.default_rng(8)
+    blob = rng.integers(0, 256, 1024 * 16 + 64, dtype=np.uint8)
+    base = dev_blob(blob)
+    k = np.arange(period, dtype=np.int64)
+    table_d = mk_descs((k % 1024) * 16 + k % 3, 20 + k % 7, (k * 2654435761) & 0xFFFFFFFF)
+    table = pyoracle.batch(blob, table_d).astype(np.int32)
+    # descriptors built on the GPU: row i = table_d[i % period], by prefix
+    # copies of whole periods (plain slices: no index kernels over 2^32 rows)
+    dt = torch.from_numpy(table_d.view(np.int64).reshape(period, 2).copy()).cuda()
+    descs = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    descs[:period] = dt
+    chunk = period * (1 << 15)  # ~235 M rows, 3.8 GB per copy
+    filled = period
+    while filled < n:
+        c = min(filled, n - filled, chunk)
+        descs[filled:filled + c] = descs[:c]
+        filled += c
+    out = torch.empty(n, dtype=torch.int16, device="cuda")
+    tt = torch.from_numpy(table).cuda()
+    for variant in [(lvlip.KERNEL_AUTO, 0, 0), (lvlip.KERNEL_WAVE, 2, 0)]:
+        out.fill_(0)
+        lvlip.batch_torch(base, descs, out, kernel=variant[0], unroll=variant[1])
+        torch.cuda.synchronize()
+        for lo in range(0, n, chunk):
+            hi = min(n, lo + chunk)
+            full = (hi - lo) // period
+            got = out[lo:lo + full * period].view(full, period).to(torch.int32) & 0xFFFF
+            bad = int((got != tt.view(1, period)).sum())
+            if hi - lo > full * period:
+                tail = out[lo + full * period:hi].to(torch.int32) & 0xFFFF
+                bad += int((tail != tt[: tail.numel()]).sum())
+            assert bad == 0, (variant, lo, bad)
+    del descs, out, base, dt, tt
+    torch.cuda.empty_cache()
