@@ -113,6 +113,33 @@ uint32_t lvlip_icmp_echo_reply_csum(uint16_t req_csum);
  * request. */
 uint32_t lvlip_icmp_echo_reply_fill(lvlip_frame *frames, uint32_t n);
 
+/* ---- f1/f2 on device-resident frames ------------------------------------ */
+
+/* Frames already in HBM (a receive ring filled by a GPU-direct NIC, or frames
+ * built on the GPU): one frame = `len` bytes at base + offset, Ethernet header
+ * first.  All three steps (plan, checksum batch, apply) run as kernels on the
+ * caller's stream; nothing returns to the host.  Pointers are device
+ * pointers; `base` is 16-B aligned and readable up to the last frame's end
+ * rounded up to 16 B.  `workspace` holds lvlip_frames_workspace_bytes(n)
+ * bytes of device memory, 16-B aligned. */
+typedef struct lvlip_frame_desc {
+    uint64_t offset;
+    uint32_t len;
+    uint32_t reserved;  /* 0 */
+} lvlip_frame_desc;
+
+size_t lvlip_frames_workspace_bytes(uint32_t n);
+
+/* verdict[i] as lvlip_rx_verify (same decisions, same flags). */
+int lvlip_rx_verify_dev(const void *base, const lvlip_frame_desc *frames, uint32_t n,
+                        uint32_t flags, uint8_t *verdict, void *workspace, void *stream);
+
+/* Fills the TCP/ICMP and IPv4 checksums in place, as lvlip_tx_checksum.  A
+ * malformed frame (not IPv4, short) is left untouched and gets status 0 (1 =
+ * filled); status may be NULL. */
+int lvlip_tx_checksum_dev(void *base, const lvlip_frame_desc *frames, uint32_t n,
+                          uint8_t *status, void *workspace, void *stream);
+
 /* RFC 1071 pseudo-header seed with the carries folded back (for RX verify of
  * checksums produced by RFC-correct peers). */
 uint32_t lvlip_pseudo_sum_rfc(uint32_t saddr, uint32_t daddr, uint8_t proto,

@@ -983,6 +983,13 @@ int hip_fail(hipError_t e, const char* what) {
     return LVLIP_EHIP;
 }
 
+}  // namespace
+
+// Shared with skb_dev.hip (hidden: -fvisibility=hidden keeps it internal).
+int lvlip_internal_hip_fail(hipError_t e, const char* what) { return hip_fail(e, what); }
+
+namespace {
+
 struct DevInfo {
     std::atomic<int> cus{0};
 };

@@ -146,6 +146,12 @@ SIGNATURES = {
     "lvlip_tx_apply": (None, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     "lvlip_icmp_echo_reply_csum": (ctypes.c_uint32, [ctypes.c_uint16]),
     "lvlip_icmp_echo_reply_fill": (ctypes.c_uint32, [ctypes.POINTER(Frame), ctypes.c_uint32]),
+    "lvlip_frames_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint32]),
+    "lvlip_rx_verify_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
+    "lvlip_tx_checksum_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "lvlip_pseudo_sum_rfc": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8,
                                                ctypes.c_uint16]),
     "lvlip_abi_version": (ctypes.c_int, []),
@@ -322,6 +328,64 @@ def tx_plan(frames):
 
 
 CSUM_RECOMPUTE = 0xFFFFFFFF
+
+# struct lvlip_frame_desc {u64 offset; u32 len; u32 reserved;}  (include/lvlip_skb.h)
+FRAME_DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("reserved", "<u4")])
+
+
+def pack_frames(frames, align_mod: int = 16, seed: int = 0):
+    """Lay frames end to end in one uint8 array (each starting at a random
+    offset mod `align_mod`), for the device-resident frame API.  Returns
+    (buffer, FRAME_DESC_DTYPE descriptors)."""
+    rng = np.random.default_rng(seed)
+    offs, pos = [], 0
+    for f in frames:
+        pos += int(rng.integers(0, align_mod)) if align_mod > 1 else 0
+        offs.append(pos)
+        pos += len(f)
+    buf = np.zeros((pos + 64 + 15) & ~15, dtype=np.uint8)
+    d = np.zeros(len(frames), dtype=FRAME_DESC_DTYPE)
+    for i, (o, f) in enumerate(zip(offs, frames)):
+        buf[o:o + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
+        d[i]["offset"], d[i]["len"] = o, len(f)
+    return buf, d
+
+
+def _frames_dev(base, fdescs):
+    import torch
+
+    n = fdescs.numel() * fdescs.element_size() // 16 if hasattr(fdescs, "numel") else len(fdescs)
+    if not hasattr(fdescs, "numel"):
+        fdescs = torch.from_numpy(np.ascontiguousarray(fdescs, dtype=FRAME_DESC_DTYPE)
+                                  .view(np.uint8).copy()).to(base.device)
+    ws = torch.empty(int(_lib.lvlip_frames_workspace_bytes(n)), dtype=torch.uint8, device=base.device)
+    return n, fdescs, ws
+
+
+def rx_verify_dev(base, fdescs, flags: int = 0, stream=None):
+    """lvlip_rx_verify_dev on frames in a CUDA uint8 tensor; returns the verdicts
+    (uint8 CUDA tensor), asynchronously on `stream` (default: current)."""
+    import torch
+
+    n, fd, ws = _frames_dev(base, fdescs)
+    verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=base.device)
+    s = stream or torch.cuda.current_stream(base.device)
+    _check(_lib.lvlip_rx_verify_dev(base.data_ptr(), fd.data_ptr(), n, flags, verdict.data_ptr(),
+                                    ws.data_ptr(), s.cuda_stream), "lvlip_rx_verify_dev")
+    return verdict[:n]
+
+
+def tx_checksum_dev(base, fdescs, stream=None):
+    """lvlip_tx_checksum_dev in place on frames in a CUDA uint8 tensor; returns
+    the per-frame status (1 filled, 0 malformed and untouched)."""
+    import torch
+
+    n, fd, ws = _frames_dev(base, fdescs)
+    status = torch.empty(max(n, 1), dtype=torch.uint8, device=base.device)
+    s = stream or torch.cuda.current_stream(base.device)
+    _check(_lib.lvlip_tx_checksum_dev(base.data_ptr(), fd.data_ptr(), n, status.data_ptr(),
+                                      ws.data_ptr(), s.cuda_stream), "lvlip_tx_checksum_dev")
+    return status[:n]
 
 
 def icmp_echo_reply_csum(req_csum: int) -> int:
