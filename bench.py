@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--sweep", action="store_true", help="also time every kernel variant (stderr)")
+    p.add_argument("--frames", action="store_true",
+                   help="diag: device-resident frame batches (TX fill, RX verify) on the mixed frames")
     p.add_argument("--origin", choices=["local", "root"], default="local",
                    help="root: the whole batch starts on rank 0's GPU and is scattered "
                         "point to point first (timed separately, diag.scatter)")
@@ -280,6 +282,8 @@ def main():
         diag["sweep"] = sweep(lvlip, torch, base, descs, out, b, stream)
     if rank == 0 and base.numel() < (1 << 34):
         diag["read_probe_GBps"] = read_probe(lvlip, torch, base, stream)
+    if rank == 0 and args.frames:
+        diag["frames_dev"] = frames_dev(lvlip, torch, dev)
     if rank == 0 and args.e2e:
         diag["e2e_host_GBps"] = e2e(lvlip, b, base)
         diag["latency_us"] = latency(lvlip, torch, dev)
@@ -344,6 +348,49 @@ def sweep(lvlip, torch, base, descs, out, b, stream):
             res.setdefault(key, []).append(round(b.algo_bytes / ms / 1e6, 1))
     for k, v in res.items():
         log(f"sweep {k:18s} GB/s {v}")
+    return res
+
+
+def frames_dev(lvlip, torch, dev):
+    """Device-resident frame batches (diagnostic, include/lvlip_skb.h): the mixed
+    config's 2M frames made valid IPv4/TCP/ICMP frames in HBM, then TX fill,
+    RX verify (header) and RX verify with L4, each timed with HIP events on
+    the launch stream.  GB/s counts the checksummed bytes of each call."""
+    import workloads
+
+    b = workloads.make("mixed")
+    base, _, _ = workloads.to_device(b, dev)
+    hdr = b.descs[0::2]
+    pay = b.descs[1::2]
+    n = hdr.size
+    fstart = torch.from_numpy((hdr["offset"] - 14).astype(np.int64)).to(dev)
+    iplen = torch.from_numpy((20 + pay["len"]).astype(np.int64)).to(dev)
+    proto = torch.from_numpy(np.where(pay["start_sum"] != 0, 6, 1).astype(np.int64)).to(dev)
+
+    def put(k, vals):
+        base[fstart + k] = vals.to(torch.uint8) if torch.is_tensor(vals) else vals
+
+    put(12, 0x08), put(13, 0x00), put(14, 0x45), put(15, 0)
+    put(16, iplen >> 8), put(17, iplen & 0xFF), put(22, 64), put(23, proto)
+    fd = np.zeros(n, dtype=lvlip.FRAME_DESC_DTYPE)
+    fd["offset"] = hdr["offset"] - 14
+    fd["len"] = 34 + pay["len"]
+    fdt = torch.from_numpy(fd.view(np.uint8).copy()).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    l4_bytes = int(pay["len"].sum())
+    res = {}
+    for name, fn, nbytes in (
+            ("tx_fill", lambda: lvlip.tx_checksum_dev(base, fdt, stream=stream), 20 * n + l4_bytes),
+            ("rx_header", lambda: lvlip.rx_verify_dev(base, fdt, 0, stream=stream), 20 * n),
+            ("rx_header_l4", lambda: lvlip.rx_verify_dev(base, fdt, lvlip.RX_VERIFY_L4, stream=stream),
+             20 * n + l4_bytes)):
+        ms = timed(torch, fn, stream, reps=10)
+        res[name] = {"ms": round(ms, 4), "Mframes_per_s": round(n / ms / 1e3, 1),
+                     "GBps": round(nbytes / ms / 1e6, 1)}
+    v = lvlip.rx_verify_dev(base, fdt, 0, stream=stream)
+    torch.cuda.synchronize(dev)
+    res["rx_header_all_ok"] = bool((v == lvlip.RX_OK).all())
+    log("device-resident frames", res)
     return res
 
 

@@ -4,8 +4,9 @@
 // Same decisions as skb_batch.c (which cites the reference line of each), as
 // three stream-ordered steps with no host round trip:
 //   plan   one thread per frame parses its Ethernet/IPv4 header bytes and
-//          writes two checksum descriptors at fixed slots 2i, 2i+1 (an unused
-//          slot is an empty descriptor) plus a plan word,
+//          writes its checksum descriptors at fixed slots (2i, 2i+1 when an L4
+//          entry may exist, else i; an unused slot is an empty descriptor) plus
+//          a plan word,
 //   batch  lvlip_csum_batch_dev_ex over the 2n descriptors (AUTO: the flat
 //          sweep, as the entries are 20-60 B headers next to payloads),
 //   apply  one thread per frame turns its two results into a verdict (RX) or
@@ -95,22 +96,26 @@ __global__ __launch_bounds__(256) void k_rx_plan(const uint8_t* __restrict__ bas
             }
         }
     }
-    descs[2 * i] = d0;
-    descs[2 * i + 1] = d1;
+    if (flags & LVLIP_RX_VERIFY_L4) {
+        descs[2 * i] = d0;
+        descs[2 * i + 1] = d1;
+    } else {
+        descs[i] = d0;  // header entries only: one slot per frame
+    }
     plan[i] = w | v;
 }
 
 __global__ __launch_bounds__(256) void k_rx_apply(const uint32_t* __restrict__ plan,
                                                   const uint16_t* __restrict__ res, uint32_t n,
-                                                  uint8_t* __restrict__ verdict) {
+                                                  uint32_t slots, uint8_t* __restrict__ verdict) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t w = plan[i];
     uint32_t v = w & 0xffu;
     if (w & kHasHdr) {
-        if (res[2 * i] != 0u)
+        if (res[slots * i] != 0u)
             v = LVLIP_RX_BAD_CSUM;
-        else if ((w & kHasL4) && res[2 * i + 1] != 0u && v == 0u)
+        else if ((w & kHasL4) && res[slots * i + 1] != 0u && v == 0u)
             v = LVLIP_RX_BAD_L4;
         v = v == 0u ? (uint32_t)LVLIP_RX_OK : (v & ~kPending);
     }
@@ -216,10 +221,11 @@ int lvlip_rx_verify_dev(const void* base, const lvlip_frame_desc* frames, uint32
                        w.descs, w.plan);
     int rc = launched("k_rx_plan");
     if (rc != LVLIP_OK) return rc;
-    lvlip_launch_cfg cfg = {LVLIP_KERNEL_AUTO, 0, 0, 0};  // headers + payloads: the flat sweep
-    rc = lvlip_csum_batch_dev_ex(base, w.descs, 2u * n, w.res, stream, &cfg);
+    const uint32_t slots = (flags & LVLIP_RX_VERIFY_L4) ? 2u : 1u;
+    lvlip_launch_cfg cfg = {LVLIP_KERNEL_AUTO, 0, 0, 0};  // headers (+ payloads): the flat sweep
+    rc = lvlip_csum_batch_dev_ex(base, w.descs, slots * n, w.res, stream, &cfg);
     if (rc != LVLIP_OK) return rc;
-    hipLaunchKernelGGL(k_rx_apply, dim3(grid), dim3(256), 0, s, w.plan, w.res, n, verdict);
+    hipLaunchKernelGGL(k_rx_apply, dim3(grid), dim3(256), 0, s, w.plan, w.res, n, slots, verdict);
     return launched("k_rx_apply");
 }
 
