@@ -127,6 +127,8 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
 #define LVLIP_KERNEL_WAVE_LDS    2  /* one wave per packet, LDS-DMA staging (A/B)  */
 #define LVLIP_KERNEL_FLAT        3  /* chunk-balanced tile sweep (ragged batches)  */
 #define LVLIP_KERNEL_WAVE_SIMPLE 4  /* one wave per packet, one launch wave each   */
+#define LVLIP_KERNEL_WAVE_STATIC 6  /* WAVE with a static split only (A/B)        */
+#define LVLIP_KERNEL_WAVE_DYN    7  /* WAVE with a dynamic cross-XCD tail (A/B)   */
 
 typedef struct lvlip_launch_cfg {
     int32_t  kernel;        /* LVLIP_KERNEL_*                               */

@@ -38,8 +38,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <vector>
 
 #include "lvlip_csum.h"
 
@@ -337,20 +339,42 @@ __device__ __forceinline__ void piece_wait(u32x4& a, u32x4& b) {
 // piece.  R pieces are in flight; the oldest is retired by vmcnt(2*(R-1)).
 // (r01 profile of a per-1KiB-slot ring: ~130 SALU per packet, the CU's scalar
 // unit ~80 % busy and the kernel SALU-bound; this layout cuts that ~3x.)
-template <int R, int POL = 0>
-__global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base,
+// SLEEPER (diagnostic, LVLIP_STREAM_SLEEPER=1): a fifth wave per workgroup that
+// only sleeps until the four streamers are done — the shape of k_stream_dyn's
+// claimer, to price the workgroup shape alone.
+template <int R, int POL = 0, bool SLEEPER = false, int PAD = 0>
+__global__ __launch_bounds__(SLEEPER ? 320 : 256) void k_stream(const uint8_t* __restrict__ base,
                                                 const lvlip_csum_desc* __restrict__ descs,
                                                 uint32_t n, uint32_t per_wave,
                                                 uint16_t* __restrict__ out) {
     __shared__ uint4 s_win[SW_WAVES][2][64];
+    __shared__ uint32_t s_done;
     constexpr uint32_t END = 0xffffffffu;
     constexpr uint32_t PIECE = 2048u;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lane16 = lane * 16u;
     const uint32_t wid = uniform(threadIdx.x >> 6);
+    if (SLEEPER) {
+        if (threadIdx.x == 0) s_done = 0;
+        __syncthreads();
+        if (wid == SW_WAVES) {
+            while (__hip_atomic_load(&s_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < SW_WAVES)
+                __builtin_amdgcn_s_sleep(127);
+            return;
+        }
+    }
+    auto sleeper_done = [&]() {
+        if (SLEEPER && lane == 0) {
+            __hip_atomic_fetch_add(&s_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            asm volatile("s_wakeup" ::: "memory");
+        }
+    };
     const uint32_t wave = uniform(blockIdx.x * SW_WAVES + wid);
     const uint64_t lo64 = (uint64_t)wave * per_wave;
-    if (lo64 >= n) return;
+    if (lo64 >= n) {
+        sleeper_done();
+        return;
+    }
     const uint32_t p_lo = (uint32_t)lo64;
     const uint32_t p_hi = (uint32_t)min<uint64_t>(lo64 + per_wave, (uint64_t)n);
 
@@ -461,6 +485,12 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
         acc = dot2_acc(y.z, acc);
         acc = dot2_acc(y.w, acc);
         if (meta & 1u) {
+            if (PAD > 0) {  // diagnostic: PAD dependent SALU per packet (LVLIP_STREAM_PAD)
+                uint32_t z = meta;
+#pragma unroll
+                for (int i = 0; i < PAD; ++i) asm volatile("s_add_u32 %0, %0, 1" : "+s"(z) :: "scc");
+                asm volatile("" :: "s"(z));
+            }
             const uint32_t w = wave_sum_dpp(acc);
             acc = 0;
             const uint32_t k = s_pkt[r] - gc;
@@ -494,6 +524,390 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this wave left in flight
+    sleeper_done();
+}
+
+// ------------------------------------- k_stream_dyn (k_stream + dynamic tail) --
+//
+// k_stream's static split leaves the kernel waiting on the slowest XCD: under a
+// full-chip stream the eight XCDs drain equal shares 5-9 % apart
+// (scripts/lab_timeline.py: waves of one XCD end within ~10 us of each other,
+// whole XCDs 20-30 us apart on 1.5 GB).  Here each streaming wave first sweeps
+// a static segment (most of its share), then takes further segments of `chunk`
+// packets claimed from eight pools, so fast XCDs take the work slow ones have
+// not reached:
+//
+//   pool q = packets [t0 + q*plen, min(t0 + (q+1)*plen, n)), head ctr[q*32]
+//   claim  = atomic add on a head; [old, old + k*chunk) ∩ pool, or "empty"
+//
+// Who claims: a workgroup is 4 streaming waves + 1 claimer wave.  The claimer
+// does every global atomic and hands segments to its streamers through LDS
+// queues (one segment kept queued per streamer).  A streamer's vector-memory
+// counter therefore never holds an atomic: vmcnt retires in issue order, so a
+// contended atomic in a streamer's queue would stall its load ring behind it
+// (measured: a streamer-side claim version ran at 3.6 TB/s against 6.6 static).
+//
+//   * the claimer starts on pool XCC_ID (speed only: correctness never depends
+//     on placement; every packet belongs to exactly one static segment or claim)
+//   * one atomic per claimer round covers every streamer that needs a segment
+//   * a pool that comes back short is marked in ctr[8*32] (a hint for other
+//     claimers, read with sc0 sc1), and the claimer moves to the next pool;
+//     when all eight are empty it posts "end" to its streamers
+//   * the last claimer to leave (exit counter ctr[9*32]) zeroes the heads, mask
+//     and counter, so the next launch on the same block starts clean
+//
+// Windows: up to 64 packets of one segment; descriptors arrive by LDS-DMA into
+// the other half of the wave's double buffer while the current one is swept.
+// Results gather per window and leave as one store of up to 64 x 2 B.
+struct TailArgs {
+    uint32_t* ctr;    // counter block (zeroed before the first launch)
+    uint32_t t0;      // first pooled packet (= streaming waves * per_wave)
+    uint32_t plen;    // packets per pool
+    uint32_t chunk;   // packets per claim
+    uint32_t nblocks; // workgroups in the grid
+    unsigned long long* trace;  // diagnostics only (LVLIP_TAIL_TRACE): 8 u64 per streamer, or null
+};
+
+constexpr uint32_t TAIL_MASK = 8u * 32u;  // ctr index of the empty-pool mask
+constexpr uint32_t TAIL_EXIT = 9u * 32u;  // ctr index of the exit counter
+constexpr uint32_t TAIL_WORDS = 10u * 32u;
+constexpr int DYN_THREADS = (SW_WAVES + 1) * 64;
+constexpr uint32_t TQ = 4;  // queue slots per streamer (one is kept filled)
+
+__device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int R, int POL = 0>
+__global__ __launch_bounds__(DYN_THREADS) void k_stream_dyn(const uint8_t* __restrict__ base,
+                                                            const lvlip_csum_desc* __restrict__ descs,
+                                                            uint32_t n, uint32_t per_wave, TailArgs ta,
+                                                            uint16_t* __restrict__ out) {
+    __shared__ uint4 s_win[SW_WAVES][2][64];
+    // per streamer: segment ring [lo, hi) x TQ, tail (claimer), head (streamer), end flag
+    __shared__ uint32_t q_lo[SW_WAVES][TQ], q_hi[SW_WAVES][TQ];
+    __shared__ uint32_t q_tail[SW_WAVES], q_head[SW_WAVES], q_end[SW_WAVES];
+    constexpr uint32_t END = 0xffffffffu;
+    constexpr uint32_t PIECE = 2048u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = uniform(threadIdx.x >> 6);
+    if (threadIdx.x < SW_WAVES) {
+        q_tail[threadIdx.x] = 0;
+        q_head[threadIdx.x] = 0;
+        q_end[threadIdx.x] = 0;
+    }
+    __syncthreads();
+
+    auto pool_lo = [&](uint32_t q) { return ta.t0 + q * ta.plen; };
+    auto pool_hi = [&](uint32_t q) {
+        return (uint32_t)min<uint64_t>((uint64_t)ta.t0 + (uint64_t)(q + 1u) * ta.plen, (uint64_t)n);
+    };
+
+    // ------------------------------------------------------------ claimer --
+    if (wid == SW_WAVES) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        uint32_t q = xcc & 7u, empty = 0;  // current pool, pools known empty (uniform)
+        uint32_t pushed = 0;               // lane l < 4: segments pushed to streamer l
+        bool fin = lane >= SW_WAVES;       // lane l < 4: "end" posted to streamer l
+        for (;;) {
+            const bool need = !fin && pushed - lds_load(&q_head[lane & (SW_WAVES - 1)]) < 1u;
+            const uint64_t needm = __builtin_amdgcn_ballot_w64(need);
+            if (!needm) {
+                if (!__builtin_amdgcn_ballot_w64(!fin)) break;
+                // idle: sleep long (a polling claimer takes issue slots from its
+                // streamers); a streamer's pop wakes it (s_wakeup)
+                __builtin_amdgcn_s_sleep(127);
+                continue;
+            }
+            if (empty == 0xffu) {  // nothing left anywhere: post "end"
+                if (!fin) lds_store(&q_end[lane], 1u);
+                fin = true;
+                continue;
+            }
+            const uint32_t m = (uint32_t)__popcll(needm);
+            uint32_t old = 0;
+            if (lane == 0) old = atomicAdd(ta.ctr + q * 32u, m * ta.chunk);
+            old = uniform(old);
+            const uint32_t pl = pool_lo(q), ph = pool_hi(q);
+            const uint32_t len = ph > pl ? ph - pl : 0u;
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+            const uint64_t st = (uint64_t)old + (uint64_t)r * ta.chunk;
+            if (need && st < len) {
+                const uint32_t slot = pushed % TQ;
+                lds_store(&q_lo[lane][slot], pl + (uint32_t)st);
+                lds_store(&q_hi[lane][slot], pl + (uint32_t)min<uint64_t>(st + ta.chunk, len));
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);  // segment before tail
+                lds_store(&q_tail[lane], pushed + 1u);
+                ++pushed;
+            }
+            if ((uint64_t)old + (uint64_t)m * ta.chunk >= len) {
+                // pool q is used up: tell other claimers, learn what they know
+                uint32_t g = 0;
+                if (lane == 0) {
+                    atomicOr(ta.ctr + TAIL_MASK, 1u << q);
+                    const uint32_t* mp = ta.ctr + TAIL_MASK;
+                    asm volatile("global_load_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                                 : "=v"(g) : "v"(mp) : "memory");
+                }
+                empty |= (1u << q) | uniform(g);
+                for (uint32_t t = 1; t <= 8u && (empty >> q) & 1u; ++t) q = (q + 1u) & 7u;
+            }
+        }
+        if (lane == 0 && atomicAdd(ta.ctr + TAIL_EXIT, 1u) == ta.nblocks - 1u) {
+            for (uint32_t k = 0; k < 8u; ++k) atomicExch(ta.ctr + k * 32u, 0u);
+            atomicExch(ta.ctr + TAIL_MASK, 0u);
+            atomicExch(ta.ctr + TAIL_EXIT, 0u);
+        }
+        return;
+    }
+
+    // ---------------------------------------------------------- streamers --
+    // Loop-carried scalars are kept to what every packet needs (ip, io, the
+    // window bounds, the packet's resource words); the segment and next-window
+    // state changes once per window and lives in lanes of one VGPR (ST_*), so
+    // the compiler has no SGPR phis to shuffle on the per-packet path.
+    enum { ST_SEG_HI = 0, ST_X_LO, ST_X_HI, ST_X_SEG_HI, ST_X_VALID, ST_POPPED, ST_WB };
+    const uint32_t lane16 = lane * 16u;
+    const uint32_t wave = uniform(blockIdx.x * SW_WAVES + wid);
+    const unsigned long long t_start = ta.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+
+    // static segment (per_wave >= 128 packets: launcher), ends at or before t0
+    const uint32_t s_lo = (uint32_t)min<uint64_t>((uint64_t)wave * per_wave, (uint64_t)n);
+    const uint32_t s_hi = (uint32_t)min<uint64_t>((uint64_t)wave * per_wave + per_wave,
+                                                  (uint64_t)min(ta.t0, n));
+
+    uint32_t st = 0;  // VGPR: lane i = field i
+    auto get = [&](int f) { return (uint32_t)__builtin_amdgcn_readlane((int)st, f); };
+    auto put = [&](int f, uint32_t v) {
+        const uint32_t u = uniform(v);  // LDS-loaded values are not known uniform
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(st) : "s"(u), "n"(f));
+    };
+
+    // next segment from the claimer.  The wait for a non-empty queue (or "end")
+    // is one asm block: a loop in the C++ control flow here would sit inside
+    // the ring loop and cost register copies on every packet (measured).
+    const uint32_t a_tail = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&q_tail[wid];
+    const uint32_t a_end = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&q_end[wid];
+    auto pop = [&](uint32_t& lo, uint32_t& hi) -> bool {
+        const uint32_t popped = get(ST_POPPED);
+        uint32_t vt, ve, tail, fin;
+        asm volatile(
+            "1:\n\t"
+            "ds_read_b32 %0, %4\n\t"
+            "ds_read_b32 %1, %5\n\t"
+            "s_waitcnt lgkmcnt(0)\n\t"
+            "v_readfirstlane_b32 %2, %0\n\t"
+            "v_readfirstlane_b32 %3, %1\n\t"
+            "s_nop 1\n\t"
+            "s_cmp_gt_u32 %2, %6\n\t"
+            "s_cbranch_scc1 2f\n\t"
+            "s_cmp_lg_u32 %3, 0\n\t"
+            "s_cbranch_scc1 2f\n\t"
+            "s_wakeup\n\t"
+            "s_sleep 1\n\t"
+            "s_branch 1b\n"
+            "2:"
+            : "=&v"(vt), "=&v"(ve), "=&s"(tail), "=&s"(fin)
+            : "v"(a_tail), "v"(a_end), "s"(popped)
+            : "memory", "scc");
+        if (tail <= popped) {
+            // "end" was seen; the claimer writes tail before end, so a fresh
+            // read of tail is final
+            tail = uniform(lds_load(&q_tail[wid]));
+            if (tail <= popped) return false;
+        }
+        const uint32_t slot = popped % TQ;
+        lo = lds_load(&q_lo[wid][slot]);
+        hi = lds_load(&q_hi[wid][slot]);
+        put(ST_POPPED, popped + 1u);
+        lds_store(&q_head[wid], popped + 1u);
+        asm volatile("s_wakeup" ::: "memory");  // the claimer refills the queue
+        return true;
+    };
+
+    // the window after [w_lo, w_hi) -> ST_X_*
+    auto plan_next = [&](uint32_t w_hi) {
+        const uint32_t seg_hi = get(ST_SEG_HI);
+        if (w_hi < seg_hi) {
+            put(ST_X_LO, w_hi);
+            put(ST_X_HI, min(w_hi + 64u, seg_hi));
+            put(ST_X_SEG_HI, seg_hi);
+            put(ST_X_VALID, 1u);
+        } else {
+            uint32_t lo = 0, hi = 0;
+            const bool ok = pop(lo, hi);
+            put(ST_X_LO, lo);
+            put(ST_X_HI, min(lo + 64u, hi));
+            put(ST_X_SEG_HI, hi);
+            put(ST_X_VALID, ok ? 1u : 0u);
+        }
+    };
+
+    uint32_t w_lo = s_lo, w_hi = min(s_lo + 64u, s_hi);
+    put(ST_SEG_HI, s_hi);
+    put(ST_POPPED, 0u);
+    put(ST_WB, 0u);
+    fetch_window(descs, w_lo, n, lane, s_win[wid][0]);
+    plan_next(w_hi);
+    if (get(ST_X_VALID)) fetch_window(descs, get(ST_X_LO), n, lane, s_win[wid][1]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    uint32_t m_x, m_y, m_z, m_t, m_s;
+    auto load_window_meta = [&](uint32_t b) {
+        const uint4 d = s_win[wid][b][lane];
+        const PacketMeta pm = packet_meta(base, u32x4{d.x, d.y, d.z, d.w});
+        m_x = pm.srd.x;
+        m_y = pm.srd.y;
+        m_z = pm.srd.z;
+        m_t = pm.tinfo;
+        m_s = pm.start;
+    };
+    load_window_meta(0);
+
+    uint32_t ip = w_lo, io = 0;
+    u32x4 srd;
+    uint32_t tinfo, start;
+    auto pull = [&](uint32_t k) {
+        srd.x = (uint32_t)__builtin_amdgcn_readlane((int)m_x, (int)k);
+        srd.y = (uint32_t)__builtin_amdgcn_readlane((int)m_y, (int)k);
+        srd.z = (uint32_t)__builtin_amdgcn_readlane((int)m_z, (int)k);
+        srd.w = SRD_WORD3;
+        tinfo = (uint32_t)__builtin_amdgcn_readlane((int)m_t, (int)k);
+        start = (uint32_t)__builtin_amdgcn_readlane((int)m_s, (int)k);
+    };
+    pull(0);
+    bool live = true;
+
+    uint32_t res_w = 0, res_s = 0;
+    uint32_t acc = 0;
+    uint32_t gc = w_lo;  // consume side: first packet of the window being gathered
+    u32x4 va[R], vb[R];
+    // per piece: packet (END past the work); meta = last | (len & 3) << 1 |
+    // (offset of the last dword in the piece) << 3 | window-last << 14
+    uint32_t s_pkt[R], s_start[R], s_meta[R];
+
+    auto issue = [&](int r) {
+        u32x4 sr = srd;
+        if (!live) sr.z = 0;
+        const uint32_t off = lane16 + io;
+        va[r] = buffer_load_nt_asm<POL>(off, sr);
+        vb[r] = buffer_load_nt_asm<POL>(off + 1024u, sr);
+        const bool last = io + PIECE >= srd.z;
+        const bool wlast = last && ip + 1u == w_hi;
+        s_pkt[r] = live ? ip : END;
+        s_start[r] = start;
+        s_meta[r] = (uint32_t)last | ((tinfo & 3u) << 1) | ((((srd.z - 4u) - io) & 0x7FFu) << 3) |
+                    ((uint32_t)wlast << 14);
+        if (live) {
+            if (!last) {
+                io += PIECE;
+            } else {
+                ++ip;
+                io = 0;
+                if (ip == w_hi) {  // leaving the window (rare path, one merge point)
+                    if (get(ST_X_VALID)) {
+                        // the next window's DMA was followed by at least one
+                        // piece (two loads): vmcnt(2) retires it (issue order)
+                        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                        const uint32_t wb = get(ST_WB) ^ 1u;
+                        put(ST_WB, wb);
+                        w_lo = get(ST_X_LO);
+                        w_hi = get(ST_X_HI);
+                        put(ST_SEG_HI, get(ST_X_SEG_HI));
+                        load_window_meta(wb);
+                        ip = w_lo;
+                        plan_next(w_hi);
+                        if (get(ST_X_VALID)) fetch_window(descs, get(ST_X_LO), n, lane, s_win[wid][wb ^ 1u]);
+                    } else {
+                        live = false;
+                    }
+                }
+                if (live) pull(ip - w_lo);
+            }
+        }
+    };
+
+    auto consume = [&](int r) {
+        piece_wait<2 * (R - 1)>(va[r], vb[r]);
+        u32x4 x = va[r], y = vb[r];
+        const uint32_t meta = s_meta[r];
+        const uint32_t len3 = (meta >> 1) & 3u;
+        if ((meta & 1u) && len3) {
+            const uint32_t pos = (meta >> 3) & 0x7FFu;
+            const uint32_t m = (1u << (8u * len3)) - 1u;
+            const bool me = lane == ((pos >> 4) & 63u);
+            const uint32_t tk = (pos >> 2) & 3u;
+            const bool in_b = pos >= 1024u;
+            const uint32_t m0 = (me && tk == 0u) ? m : ~0u, m1 = (me && tk == 1u) ? m : ~0u;
+            const uint32_t m2 = (me && tk == 2u) ? m : ~0u, m3 = (me && tk == 3u) ? m : ~0u;
+            if (in_b) {
+                y.x &= m0; y.y &= m1; y.z &= m2; y.w &= m3;
+            } else {
+                x.x &= m0; x.y &= m1; x.z &= m2; x.w &= m3;
+            }
+        }
+        acc = dot2_acc(x.x, acc);
+        acc = dot2_acc(x.y, acc);
+        acc = dot2_acc(x.z, acc);
+        acc = dot2_acc(x.w, acc);
+        acc = dot2_acc(y.x, acc);
+        acc = dot2_acc(y.y, acc);
+        acc = dot2_acc(y.z, acc);
+        acc = dot2_acc(y.w, acc);
+        if (meta & 1u) {
+            const uint32_t w = wave_sum_dpp(acc);
+            acc = 0;
+            const uint32_t k = s_pkt[r] - gc;
+            if (lane == k) {
+                res_w = w;
+                res_s = s_start[r];
+            }
+            if (meta & (1u << 14)) {
+                uint32_t tt = res_s + res_w;
+                tt = (tt & 0xffffu) + (tt >> 16);
+                tt = (tt & 0xffffu) + (tt >> 16);
+                if (lane <= k) out[gc + lane] = (uint16_t)~tt;
+                gc = END;  // the next window's first packet sets it
+            }
+        }
+    };
+
+#pragma unroll
+    for (int r = 0; r < R; ++r) issue(r);
+    bool done = false;
+    while (!done) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (s_pkt[r] == END) {
+                done = true;
+                break;
+            }
+            if (gc == END) gc = s_pkt[r];  // first piece of a new window
+            consume(r);
+            issue(r);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (ta.trace && lane == 0) {
+        uint32_t xid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xid));
+        unsigned long long* t = ta.trace + (uint64_t)wave * 8u;
+        t[0] = t_start;
+        t[1] = 0;
+        t[2] = __builtin_amdgcn_s_memrealtime();
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        t[3] = get(ST_POPPED);
+        t[4] = xid & 7u;
+        t[5] = s_hi - s_lo;
+        t[6] = wid;
+        t[7] = hw;
+    }
 }
 
 // ------------------------------------------------- k_wave_lds (LDS-DMA path) --
@@ -1075,10 +1489,142 @@ void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvli
         LVLIP_STREAM_POL(3)
         LVLIP_STREAM_POL(4)
 #undef LVLIP_STREAM_POL
-        default:
-            hipLaunchKernelGGL((lvlip::k_stream<U, 0>), dim3(grid), dim3(256), 0, s,
-                               (const uint8_t*)base, d, n, per_wave, out);
+        default: {
+            static const bool sleeper = getenv("LVLIP_STREAM_SLEEPER") != nullptr;  // diagnostic
+            static const bool pad = getenv("LVLIP_STREAM_PAD") != nullptr;          // diagnostic
+            if (pad)
+                hipLaunchKernelGGL((lvlip::k_stream<U, 0, false, 16>), dim3(grid), dim3(256), 0, s,
+                                   (const uint8_t*)base, d, n, per_wave, out);
+            else if (sleeper)
+                hipLaunchKernelGGL((lvlip::k_stream<U, 0, true>), dim3(grid), dim3(320), 0, s,
+                                   (const uint8_t*)base, d, n, per_wave, out);
+            else
+                hipLaunchKernelGGL((lvlip::k_stream<U, 0>), dim3(grid), dim3(256), 0, s,
+                                   (const uint8_t*)base, d, n, per_wave, out);
+        }
     }
+}
+
+// ---- dynamic tail of the stream kernel (k_stream_dyn) ----
+//
+// Counter blocks: one per (device, stream), from a per-device pool allocated
+// and zeroed once.  Launches on one stream are serialised, so they may share a
+// block (each launch's last wave zeroes it for the next).  A launch captured
+// into a HIP graph gets a block of its own that nothing else uses (a graph
+// holding a batch must not be replayed concurrently with itself, as with any
+// kernel that owns scratch).  When no block is available (pool exhausted, the
+// per-thread default stream, first use while capturing) the launch uses the
+// static split.
+constexpr int kTailSlots = 256;
+
+struct TailPool {
+    uint32_t* mem = nullptr;
+    bool failed = false;
+    int used = 0;
+    std::vector<std::pair<uintptr_t, int>> by_stream;
+};
+std::mutex g_tail_mu;
+TailPool g_tail[64];
+
+uint32_t* tail_block(int dev, hipStream_t s) {
+    if (dev < 0 || dev >= 64 || s == hipStreamPerThread) return nullptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess) return nullptr;
+    const bool capturing = cs != hipStreamCaptureStatusNone;
+    std::lock_guard<std::mutex> lk(g_tail_mu);
+    TailPool& p = g_tail[dev];
+    if (!p.mem) {
+        if (p.failed || capturing) return nullptr;
+        const size_t bytes = (size_t)kTailSlots * lvlip::TAIL_WORDS * 4u;
+        void* m = nullptr;
+        if (hipMalloc(&m, bytes) != hipSuccess || hipMemset(m, 0, bytes) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess) {
+            if (m) (void)hipFree(m);
+            p.failed = true;
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        p.mem = (uint32_t*)m;
+    }
+    if (!capturing)
+        for (const auto& e : p.by_stream)
+            if (e.first == (uintptr_t)s) return p.mem + (size_t)e.second * lvlip::TAIL_WORDS;
+    if (p.used >= kTailSlots) return nullptr;
+    const int slot = p.used++;
+    if (!capturing) p.by_stream.emplace_back((uintptr_t)s, slot);
+    return p.mem + (size_t)slot * lvlip::TAIL_WORDS;
+}
+
+// LVLIP_TAIL_PCT: share of the batch left to claims (default 0 = static split,
+// k_stream; the dynamic tail is an A/B variant until it measures faster:
+// DESIGN.md §8); LVLIP_TAIL_CHUNK: bytes per claim (default 16384).  Read once.
+int tail_pct() {
+    static const int v = [] {
+        const char* e = getenv("LVLIP_TAIL_PCT");
+        const int x = e ? atoi(e) : 0;
+        return x < 0 ? 0 : (x > 90 ? 90 : x);
+    }();
+    return v;
+}
+int tail_chunk_bytes() {
+    static const int v = [] {
+        const char* e = getenv("LVLIP_TAIL_CHUNK");
+        const int x = e ? atoi(e) : 16384;
+        return x < 1024 ? 1024 : x;
+    }();
+    return v;
+}
+
+// Returns false when the dynamic tail does not apply (caller falls back to
+// the static launch).
+template <int U>
+bool launch_stream_dyn(int waves_per_cu, hipStream_t s, const void* base,
+                       const lvlip_csum_desc* d, uint32_t n, uint16_t* out, int len_hint,
+                       bool explicit_dyn) {
+    // WAVE_DYN uses LVLIP_TAIL_PCT or 15; WAVE only when LVLIP_TAIL_PCT > 0
+    const int pct = explicit_dyn && getenv("LVLIP_TAIL_PCT") == nullptr ? 15 : tail_pct();
+    // diagnostic: LVLIP_TAIL_FORCE runs this kernel with pct 0 (static shares
+    // covering the batch, empty pools) to price the kernel's own structure
+    static const bool force = getenv("LVLIP_TAIL_FORCE") != nullptr;
+    if (pct == 0 && !force) return false;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint64_t waves = ((uint64_t)cu_count(dev) * (uint64_t)waves_per_cu + 3) & ~3ull;
+    // each streaming wave's static segment must span two windows (its first
+    // two descriptor windows are filled before it ever asks for a claim)
+    const uint64_t per_wave = pct == 0 ? ((uint64_t)n + waves - 1) / waves
+                                       : (uint64_t)n * (uint64_t)(100 - pct) / 100u / waves;
+    if (per_wave < 128) return false;
+    uint32_t* ctr = tail_block(dev, s);
+    if (!ctr) return false;
+    const uint64_t t0 = std::min<uint64_t>(per_wave * waves, n);
+    const int hint = len_hint > 0 ? len_hint : 1500;
+    lvlip::TailArgs ta;
+    ta.ctr = ctr;
+    ta.t0 = (uint32_t)t0;
+    ta.plen = (uint32_t)(((uint64_t)n - t0 + 7u) / 8u);
+    ta.chunk = (uint32_t)std::max(1, tail_chunk_bytes() / hint);
+    ta.nblocks = (uint32_t)(waves / 4);
+    static unsigned long long* const trace = [] {
+        const char* e = getenv("LVLIP_TAIL_TRACE");  // device address (diagnostics)
+        return e ? (unsigned long long*)(uintptr_t)strtoull(e, nullptr, 0) : nullptr;
+    }();
+    ta.trace = trace;
+    const uint32_t grid = (uint32_t)(waves / 4);
+    const uint32_t pw = (uint32_t)per_wave;
+    switch (load_policy()) {
+#define LVLIP_DYN_POL(P)                                                                 \
+    case P:                                                                              \
+        hipLaunchKernelGGL((lvlip::k_stream_dyn<U, P>), dim3(grid), dim3(lvlip::DYN_THREADS), 0, s, \
+                           (const uint8_t*)base, d, n, pw, ta, out);                     \
+        break;
+        LVLIP_DYN_POL(1)
+#undef LVLIP_DYN_POL
+        default:
+            hipLaunchKernelGGL((lvlip::k_stream_dyn<U, 0>), dim3(grid), dim3(lvlip::DYN_THREADS), 0, s,
+                               (const uint8_t*)base, d, n, pw, ta, out);
+    }
+    return true;
 }
 
 template <int U>
@@ -1138,14 +1684,31 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
     }
 
     switch (kernel) {
-        case LVLIP_KERNEL_WAVE: {
-            // unroll = 2-KiB pieces in flight per wave (2 = up to 4 KiB)
+        case LVLIP_KERNEL_WAVE:
+        case LVLIP_KERNEL_WAVE_STATIC:
+        case LVLIP_KERNEL_WAVE_DYN: {
+            // unroll = 2-KiB pieces in flight per wave (2 = up to 4 KiB).
+            // WAVE_STATIC: static split (k_stream); WAVE_DYN: dynamic tail
+            // (k_stream_dyn) where it applies; WAVE: static unless
+            // LVLIP_TAIL_PCT > 0 (DESIGN.md §8 has the measurements).
             if (unroll <= 0) unroll = 2;
             const int w = wpc > 0 ? wpc : 16;
+            const bool dyn = kernel != LVLIP_KERNEL_WAVE_STATIC;
+            const bool xd = kernel == LVLIP_KERNEL_WAVE_DYN;
+            const int hint = cfg ? cfg->len_hint : 0;
             switch (unroll) {
-                case 2: launch_stream<2>(w, s, base, descs, n, out); break;
-                case 3: launch_stream<3>(w, s, base, descs, n, out); break;
-                case 4: launch_stream<4>(w, s, base, descs, n, out); break;
+                case 2:
+                    if (!dyn || !launch_stream_dyn<2>(w, s, base, descs, n, out, hint, xd))
+                        launch_stream<2>(w, s, base, descs, n, out);
+                    break;
+                case 3:
+                    if (!dyn || !launch_stream_dyn<3>(w, s, base, descs, n, out, hint, xd))
+                        launch_stream<3>(w, s, base, descs, n, out);
+                    break;
+                case 4:
+                    if (!dyn || !launch_stream_dyn<4>(w, s, base, descs, n, out, hint, xd))
+                        launch_stream<4>(w, s, base, descs, n, out);
+                    break;
                 default: return LVLIP_EINVAL;
             }
             break;

@@ -114,6 +114,84 @@ __global__ __launch_bounds__(256) void k_probe_lds(const uint4* __restrict__ src
     if (lane == 0) atomicAdd(sink, acc);
 }
 
+// Timeline probe: where the time of a streaming read goes (launch ramp, steady
+// state, tail).  Wave-contiguous ranges (DYN = false, MODE 2's shape) or
+// granules of `gp` 1-KiB pieces claimed from 8 per-XCD queues (DYN = true:
+// queue q holds granules q, q+8, ...; a wave starts on its own XCD's queue and
+// moves to the next queue when that one is empty; the next claim is issued
+// before the current granule is read).  With tl != null lane 0 of every wave
+// writes {t_start, t_end, xcc | hw_id << 8, claims} (s_memrealtime, 100 MHz).
+template <int U, bool DYN>
+__global__ __launch_bounds__(256) void k_probe_tl(const uint4* __restrict__ src, uint64_t pieces,
+                                                  uint32_t gp, uint32_t* __restrict__ ctr,
+                                                  unsigned long long* __restrict__ tl,
+                                                  uint32_t* __restrict__ sink) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t acc = 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + wid;
+    uint32_t xcc, hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    xcc &= 7u;
+    uint32_t claims = 0;
+    auto sweep = [&](uint64_t lo, uint64_t hi) {
+        uint64_t p = lo;
+        for (; p + U <= hi; p += U) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ld<true>(src + (p + u) * 64 + lane);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += words(v[u]);
+        }
+        for (; p < hi; ++p) acc += words(ld<true>(src + p * 64 + lane));
+    };
+    if (!DYN) {
+        const uint64_t nw = (uint64_t)gridDim.x * wpb;
+        const uint64_t per = (pieces + nw - 1) / nw;
+        const uint64_t lo = wave * per;
+        const uint64_t hi = lo + per < pieces ? lo + per : pieces;
+        if (lo < hi) sweep(lo, hi);
+        claims = 1;
+    } else {
+        const uint64_t ngran = (pieces + gp - 1) / gp;
+        uint32_t q = xcc, tries = 0;
+        // claim: granule index or ~0 when every queue is empty
+        auto claim = [&]() -> uint64_t {
+            while (tries < 8u) {
+                uint32_t k = 0;
+                if (lane == 0) k = atomicAdd(&ctr[q * 32u], 1u);
+                k = __builtin_amdgcn_readfirstlane(k);
+                const uint64_t g = (uint64_t)k * 8u + q;
+                if (g < ngran) return g;
+                q = (q + 1u) & 7u;
+                ++tries;
+            }
+            return ~0ull;
+        };
+        uint64_t g = claim();
+        while (g != ~0ull) {
+            const uint64_t nxt = claim();
+            ++claims;
+            const uint64_t lo = g * gp;
+            const uint64_t hi = lo + gp < pieces ? lo + gp : pieces;
+            sweep(lo, hi);
+            g = nxt;
+        }
+    }
+    acc = wsum(acc);
+    if (lane == 0) atomicAdd(sink, acc);
+    if (tl && lane == 0) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        tl[wave * 4 + 0] = t0;
+        tl[wave * 4 + 1] = t1;
+        tl[wave * 4 + 2] = xcc | ((unsigned long long)hwid << 8);
+        tl[wave * 4 + 3] = claims;
+    }
+}
+
 template <int U, bool NT, int MODE>
 void go(uint32_t grid, hipStream_t s, const void* src, uint64_t n16, uint32_t* sink) {
     hipLaunchKernelGGL((k_probe<U, NT, MODE>), dim3(grid), dim3(256), 0, s, (const uint4*)src, n16,
@@ -145,6 +223,61 @@ extern "C" int lvlip_lab_probe(const void* src, uint64_t bytes, uint32_t* sink, 
         return hipGetLastError() == hipSuccess ? 0 : -3;
     }
     return -1;
+}
+
+// ctr: 8 queue heads at stride 32 u32 (zeroed by the caller before each DYN
+// launch); tl: 4 u64 per wave or null.
+extern "C" int lvlip_lab_probe_tl(const void* src, uint64_t bytes, uint32_t* sink, int dyn,
+                                  int unroll, uint32_t gp, uint32_t* ctr, unsigned long long* tl,
+                                  int blocks, void* stream) {
+    if (!src || !sink || (bytes & 1023u) || (dyn && (!ctr || gp == 0))) return -1;
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t pieces = bytes / 1024;
+    const dim3 g((uint32_t)blocks), b(256);
+#define TL(U, D) \
+    if (unroll == U && (bool)dyn == D) { hipLaunchKernelGGL((k_probe_tl<U, D>), g, b, 0, s, (const uint4*)src, pieces, gp, ctr, tl, sink); return hipGetLastError() == hipSuccess ? 0 : -3; }
+    TL(4, false) TL(4, true) TL(8, false) TL(8, true)
+#undef TL
+    return -1;
+}
+
+// ---- cross-XCD atomicity probe -----------------------------------------------
+// Every wave's lane 0 takes K tickets from one counter: MODE 0 agent-scope
+// atomicAdd (global_atomic_add ... sc0), MODE 1 system scope (... sc0 sc1),
+// MODE 2 the agent-scope add from asm with sc1 added.  The host checks that the
+// tickets are exactly 0 .. waves*K-1 (one claim per ticket, across XCDs).
+namespace {
+template <int MODE>
+__global__ __launch_bounds__(256) void k_atomics(uint32_t* ctr, uint32_t* tickets, uint32_t k) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (lane != 0) return;
+    for (uint32_t i = 0; i < k; ++i) {
+        uint32_t t;
+        if (MODE == 0) t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (MODE == 1) t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else {
+            const uint32_t one = 1u;
+            asm volatile("global_atomic_add %0, %1, %2, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                         : "=v"(t) : "v"(ctr), "v"(one) : "memory");
+        }
+        tickets[(wave * k + i) * 2] = t;
+        tickets[(wave * k + i) * 2 + 1] = xcc & 7u;
+    }
+}
+}  // namespace
+
+extern "C" int lvlip_lab_atomics(uint32_t* ctr, uint32_t* tickets, int mode, int blocks, uint32_t k,
+                                 void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 g((uint32_t)blocks), b(256);
+    if (mode == 0) hipLaunchKernelGGL(k_atomics<0>, g, b, 0, s, ctr, tickets, k);
+    else if (mode == 1) hipLaunchKernelGGL(k_atomics<1>, g, b, 0, s, ctr, tickets, k);
+    else if (mode == 2) hipLaunchKernelGGL(k_atomics<2>, g, b, 0, s, ctr, tickets, k);
+    else return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 // ---- buffer out-of-range semantics probe -------------------------------------

@@ -1,0 +1,21 @@
+#!/usr/bin/env python3
+"""Runs chosen kernels on one resident workload (for rocprofv3 passes):
+  RK_WORKLOAD=tcp1500 RK_KERNELS=wave,wave_static RK_REPS=10 python3 scripts/run_kernels.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "level-ip_amd"))
+import torch  # noqa: E402
+
+import lvlip  # noqa: E402
+import workloads  # noqa: E402
+
+b = workloads.make(os.environ.get("RK_WORKLOAD", "tcp1500"))
+base, descs, out = workloads.to_device(b)
+hint = b.algo_bytes // b.n
+for _ in range(int(os.environ.get("RK_REPS", "10"))):
+    for k in os.environ.get("RK_KERNELS", "wave,wave_static").split(","):
+        lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_NAMES[k], len_hint=hint)
+torch.cuda.synchronize()
+print("ok")

@@ -29,6 +29,8 @@ VARIANTS = [
     (lvlip.KERNEL_WAVE, 4, 0),
     (lvlip.KERNEL_WAVE, 2, 1),     # 1 wave/CU: long per-wave ranges, window refills
     (lvlip.KERNEL_WAVE, 4, 24),
+    (lvlip.KERNEL_WAVE_STATIC, 2, 0),  # stream kernel, static split only (A/B)
+    (lvlip.KERNEL_WAVE_DYN, 2, 1),     # dynamic tail where it applies (A/B)
     (lvlip.KERNEL_WAVE_SIMPLE, 1, 0),
     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0),
     (lvlip.KERNEL_WAVE_SIMPLE, 4, 8),
@@ -208,6 +210,7 @@ def test_full_size_bit_exact(name):
     assert bad.size == 0, f"{bad.size} of {b.n} differ; first {bad[:5]}"
     # size-independent property: every kernel variant agrees, and reruns are identical
     for variant in [(lvlip.KERNEL_WAVE, 4, 0), (lvlip.KERNEL_WAVE, 3, 4),
+                    (lvlip.KERNEL_WAVE_DYN, 2, 0), (lvlip.KERNEL_WAVE_DYN, 2, 8),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
                     (lvlip.KERNEL_AUTO, 0, 0)]:
@@ -391,6 +394,56 @@ def test_batch_dev_on_user_stream_and_graph():
     g.replay()
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+
+
+@pytest.mark.parametrize("name,n,hint", [("tcp1500", 60000, 1500), ("tcp1500", 60000, 16384),
+                                         ("tcp9000", 40000, 9000), ("mixed", 40000, 200),
+                                         ("mixed", 40000, 0)])
+def test_stream_dynamic_tail(name, n, hint):
+    """k_stream_dyn (the stream kernel's dynamic tail): with 1 wave per CU the
+    static segments are >= 128 packets, so claims run even at these sizes; the
+    hint sets the claim size (1500 -> 10 packets, 16384 -> 1, 200 -> 81, 0 ->
+    10).  Back-to-back launches on one stream reuse one counter block (the last
+    wave resets it), two streams run concurrently with blocks of their own, and
+    a graph replay uses a block of its own: every run must be bit-exact."""
+    b = workloads.make(name, n=n)
+    base, descs, out = workloads.to_device(b)
+    want = pyoracle.batch(base.cpu().numpy(), b.descs, threads=THREADS)
+    for wpc, unroll in [(1, 2), (1, 3), (1, 4)]:
+        for rep in range(4):
+            out.fill_(0)
+            lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_WAVE_DYN, unroll=unroll,
+                              waves_per_cu=wpc, len_hint=hint)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().view(np.uint16)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (wpc, unroll, rep, bad.size, bad[:5])
+    # two streams at once, each with its own counter block, several launches deep
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.zeros_like(out) for _ in range(6)]
+    for i, o in enumerate(outs):
+        s = s1 if i % 2 == 0 else s2
+        with torch.cuda.stream(s):
+            lvlip.batch_torch(base, descs, o, kernel=lvlip.KERNEL_WAVE_DYN, waves_per_cu=1,
+                              stream=s, len_hint=hint)
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy().view(np.uint16), want), i
+    # graph capture (a block of its own), replayed twice, then a direct launch
+    out.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_WAVE_DYN, waves_per_cu=1,
+                          stream=torch.cuda.current_stream(), len_hint=hint)
+    for _ in range(2):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_WAVE_DYN, waves_per_cu=1, len_hint=hint)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    del g
 
 
 def test_max_int_packet():

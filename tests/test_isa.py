@@ -59,6 +59,7 @@ def stream_kernels(asm):
     f = functions(asm)
     ks = {n: body for n, body in f.items() if "k_stream" in n}
     assert ks, "no k_stream instantiations found"
+    assert any("k_stream_dyn" in n for n in ks), "no k_stream_dyn instantiations found"
     return ks
 
 
@@ -89,6 +90,8 @@ def test_lds_dma_m0_sequence(asm):
 
 def test_ring_waits_are_counted_not_draining(asm):
     for name, body in stream_kernels(asm).items():
+        if "k_stream_dyn" in name:
+            continue  # test_dyn_waits_and_claims
         r = int(re.search(r"k_streamILi(\d+)E", name).group(1))  # pieces in flight
         waits = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt" in ins]
         ring = [w for w in waits if f"vmcnt({2 * (r - 1)})" in w]
@@ -102,3 +105,26 @@ def test_no_scratch(asm):
     for m in re.finditer(r"\.name:\s+(_Z\w*k_stream\w*)\n(?:.*\n){0,60}?\s+\.private_segment_fixed_size:\s+(\d+)",
                          asm):
         assert int(m.group(2)) == 0, m.group(1)
+
+
+def test_dyn_streamers_never_drain(asm):
+    """k_stream_dyn: the streamers keep k_stream's counted ring waits; the only
+    draining waits are the first window fill, the streamer exit and the
+    claimer's own waits on its atomics (a global atomic or the sc0 sc1 mask
+    read shortly before).  No AGPRs."""
+    for name, body in stream_kernels(asm).items():
+        if "k_stream_dyn" not in name:
+            continue
+        r = int(re.search(r"k_stream_dynILi(\d+)E", name).group(1))
+        waits = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt" in ins]
+        assert sum(f"vmcnt({2 * (r - 1)})" in w for w in waits) >= r, (name, waits)
+        other = 0
+        for i, ins in enumerate(body):
+            if ins.startswith("s_waitcnt") and "vmcnt(0)" in ins:
+                near = body[max(0, i - 12):i]
+                claimer = any(x.startswith("global_atomic") or
+                              (x.startswith("global_load_dword") and "sc0 sc1" in x) for x in near)
+                if not claimer:
+                    other += 1
+        assert other <= 3, (name, other)
+        assert not any(re.search(r"\ba\[?\d+", ins) for ins in body), name
