@@ -333,201 +333,7 @@ __device__ __forceinline__ void piece_wait(u32x4& a, u32x4& b) {
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
 }
 
-// The ring is organised in pieces: a piece is up to 2 KiB of one packet (two
-// 1 KiB wave-loads, always both issued; chunks past the packet read zeros), so
-// all per-piece bookkeeping is amortised over 2 KiB and a 1500-B segment is one
-// piece.  R pieces are in flight; the oldest is retired by vmcnt(2*(R-1)).
-// (r01 profile of a per-1KiB-slot ring: ~130 SALU per packet, the CU's scalar
-// unit ~80 % busy and the kernel SALU-bound; this layout cuts that ~3x.)
-// SLEEPER (diagnostic, LVLIP_STREAM_SLEEPER=1): a fifth wave per workgroup that
-// only sleeps until the four streamers are done — the shape of k_stream_dyn's
-// claimer, to price the workgroup shape alone.
-template <int R, int POL = 0, bool SLEEPER = false, int PAD = 0>
-__global__ __launch_bounds__(SLEEPER ? 320 : 256) void k_stream(const uint8_t* __restrict__ base,
-                                                const lvlip_csum_desc* __restrict__ descs,
-                                                uint32_t n, uint32_t per_wave,
-                                                uint16_t* __restrict__ out) {
-    __shared__ uint4 s_win[SW_WAVES][2][64];
-    __shared__ uint32_t s_done;
-    constexpr uint32_t END = 0xffffffffu;
-    constexpr uint32_t PIECE = 2048u;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lane16 = lane * 16u;
-    const uint32_t wid = uniform(threadIdx.x >> 6);
-    if (SLEEPER) {
-        if (threadIdx.x == 0) s_done = 0;
-        __syncthreads();
-        if (wid == SW_WAVES) {
-            while (__hip_atomic_load(&s_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < SW_WAVES)
-                __builtin_amdgcn_s_sleep(127);
-            return;
-        }
-    }
-    auto sleeper_done = [&]() {
-        if (SLEEPER && lane == 0) {
-            __hip_atomic_fetch_add(&s_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            asm volatile("s_wakeup" ::: "memory");
-        }
-    };
-    const uint32_t wave = uniform(blockIdx.x * SW_WAVES + wid);
-    const uint64_t lo64 = (uint64_t)wave * per_wave;
-    if (lo64 >= n) {
-        sleeper_done();
-        return;
-    }
-    const uint32_t p_lo = (uint32_t)lo64;
-    const uint32_t p_hi = (uint32_t)min<uint64_t>(lo64 + per_wave, (uint64_t)n);
-
-    // descriptor windows: packets [p_lo + 64w, p_lo + 64w + 64) live in s_win[wid][w & 1]
-    fetch_window(descs, p_lo, n, lane, s_win[wid][0]);
-    fetch_window(descs, p_lo + 64u, n, lane, s_win[wid][1]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-    // Packet metadata for the issue cursor's window, one packet per lane (VALU,
-    // 64 packets at a time); the issue side pulls its packet's fields with
-    // v_readlane.  (Computing them per packet on the scalar unit made the
-    // kernel SALU-bound: r01 profile.)
-    uint32_t m_x, m_y, m_z, m_t, m_s;  // srd.x, srd.y, srd.z, tinfo, start of packet (window + lane)
-    auto load_window_meta = [&](uint32_t w) {
-        const uint4 d = s_win[wid][w & 1u][lane];
-        const PacketMeta pm = packet_meta(base, u32x4{d.x, d.y, d.z, d.w});
-        m_x = pm.srd.x;
-        m_y = pm.srd.y;
-        m_z = pm.srd.z;
-        m_t = pm.tinfo;
-        m_s = pm.start;
-    };
-    load_window_meta(0);
-
-    // issue cursor: packet ip (k = ip - p_lo), byte offset io of the next piece in it
-    uint32_t ip = p_lo, io = 0;
-    u32x4 srd;
-    uint32_t tinfo, start;
-    auto pull = [&](uint32_t k) {  // k = packet index within its window
-        srd.x = (uint32_t)__builtin_amdgcn_readlane((int)m_x, (int)k);
-        srd.y = (uint32_t)__builtin_amdgcn_readlane((int)m_y, (int)k);
-        srd.z = (uint32_t)__builtin_amdgcn_readlane((int)m_z, (int)k);
-        srd.w = SRD_WORD3;
-        tinfo = (uint32_t)__builtin_amdgcn_readlane((int)m_t, (int)k);
-        start = (uint32_t)__builtin_amdgcn_readlane((int)m_s, (int)k);
-    };
-    pull(0);
-
-    // consume side: raw sums W and seeds of packets [gc, gc+64) gather in lanes
-    uint32_t gc = p_lo;
-    uint32_t res_w = 0, res_s = 0;
-    uint32_t acc = 0;
-
-    u32x4 va[R], vb[R];
-    // per piece: packet (END past the range), start_sum, and
-    // meta = last | (len & 3) << 1 | (byte offset of the last dword in the piece) << 3
-    uint32_t s_pkt[R], s_start[R], s_meta[R];
-
-    auto issue = [&](int r) {
-        const bool live = ip < p_hi;  // uniform
-        u32x4 sr = srd;
-        if (!live) sr.z = 0;  // past the range: every dword out of range -> zeros
-        const uint32_t off = lane16 + io;
-        va[r] = buffer_load_nt_asm<POL>(off, sr);
-        vb[r] = buffer_load_nt_asm<POL>(off + 1024u, sr);
-        // srd.z = round_up(len, 4): the piece is the packet's last when it reaches
-        // that (or the packet is empty)
-        const bool last = io + PIECE >= srd.z;
-        s_pkt[r] = live ? ip : END;
-        s_start[r] = start;
-        s_meta[r] = (uint32_t)last | ((tinfo & 3u) << 1) | (((srd.z - 4u) - io) << 3);
-        if (live) {
-            if (!last) {
-                io += PIECE;
-            } else {
-                ++ip;
-                io = 0;
-                if (ip < p_hi) {
-                    const uint32_t k = ip - p_lo;
-                    if ((k & 63u) == 0u) {  // entered window k/64
-                        load_window_meta(k >> 6);
-                        fetch_window(descs, ip + 64u, n, lane, s_win[wid][((k >> 6) + 1u) & 1u]);
-                    }
-                    pull(k & 63u);
-                }
-            }
-        }
-    };
-
-    auto consume = [&](int r) {
-        // Piece r's two loads are the oldest in flight: 2*(R-1) ring loads (and
-        // possibly result stores / window DMAs, which only make this stricter)
-        // were issued after them.
-        piece_wait<2 * (R - 1)>(va[r], vb[r]);
-        u32x4 x = va[r], y = vb[r];
-        const uint32_t meta = s_meta[r];
-        const uint32_t len3 = (meta >> 1) & 3u;
-        if ((meta & 1u) && len3) {  // uniform: keep bytes [0, len & 3) of the last dword
-            const uint32_t pos = meta >> 3;  // byte offset of that dword in the piece
-            const uint32_t m = (1u << (8u * len3)) - 1u;
-            const bool me = lane == ((pos >> 4) & 63u);
-            const uint32_t tk = (pos >> 2) & 3u;
-            const bool in_b = pos >= 1024u;
-            const uint32_t m0 = (me && tk == 0u) ? m : ~0u, m1 = (me && tk == 1u) ? m : ~0u;
-            const uint32_t m2 = (me && tk == 2u) ? m : ~0u, m3 = (me && tk == 3u) ? m : ~0u;
-            if (in_b) {
-                y.x &= m0; y.y &= m1; y.z &= m2; y.w &= m3;
-            } else {
-                x.x &= m0; x.y &= m1; x.z &= m2; x.w &= m3;
-            }
-        }
-        acc = dot2_acc(x.x, acc);
-        acc = dot2_acc(x.y, acc);
-        acc = dot2_acc(x.z, acc);
-        acc = dot2_acc(x.w, acc);
-        acc = dot2_acc(y.x, acc);
-        acc = dot2_acc(y.y, acc);
-        acc = dot2_acc(y.z, acc);
-        acc = dot2_acc(y.w, acc);
-        if (meta & 1u) {
-            if (PAD > 0) {  // diagnostic: PAD dependent SALU per packet (LVLIP_STREAM_PAD)
-                uint32_t z = meta;
-#pragma unroll
-                for (int i = 0; i < PAD; ++i) asm volatile("s_add_u32 %0, %0, 1" : "+s"(z) :: "scc");
-                asm volatile("" :: "s"(z));
-            }
-            const uint32_t w = wave_sum_dpp(acc);
-            acc = 0;
-            const uint32_t k = s_pkt[r] - gc;
-            if (lane == k) {
-                res_w = w;
-                res_s = s_start[r];
-            }
-            if (k == 63u || s_pkt[r] + 1u == p_hi) {
-                // fold 64 results at once (src/utils.c:46-54, per lane)
-                uint32_t tt = res_s + res_w;
-                tt = (tt & 0xffffu) + (tt >> 16);
-                tt = (tt & 0xffffu) + (tt >> 16);
-                if (lane <= k) out[gc + lane] = (uint16_t)~tt;
-                gc += 64u;
-            }
-        }
-    };
-
-#pragma unroll
-    for (int r = 0; r < R; ++r) issue(r);
-    bool done = false;
-    while (!done) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (s_pkt[r] == END) {
-                done = true;
-                break;
-            }
-            consume(r);
-            issue(r);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this wave left in flight
-    sleeper_done();
-}
-
-// ------------------------------------- k_stream_dyn (k_stream + dynamic tail) --
+// --------------------------------------- dynamic tail of k_stream (DYN = true) --
 //
 // k_stream's static split leaves the kernel waiting on the slowest XCD: under a
 // full-chip stream the eight XCDs drain equal shares 5-9 % apart
@@ -550,11 +356,11 @@ __global__ __launch_bounds__(SLEEPER ? 320 : 256) void k_stream(const uint8_t* _
 //   * the claimer starts on pool XCC_ID (speed only: correctness never depends
 //     on placement; every packet belongs to exactly one static segment or claim)
 //   * one atomic per claimer round covers every streamer that needs a segment
-//   * a pool that comes back short is marked in ctr[8*32] (a hint for other
-//     claimers, read with sc0 sc1), and the claimer moves to the next pool;
-//     when all eight are empty it posts "end" to its streamers
-//   * the last claimer to leave (exit counter ctr[9*32]) zeroes the heads, mask
-//     and counter, so the next launch on the same block starts clean
+//   * when its pool comes back short, the claimer reads all eight heads and
+//     moves to the pool with the most left; when none has any it posts "end"
+//     to its streamers (no claims on empty pools: see next_pool)
+//   * the last claimer to leave (exit counter ctr[9*32]) zeroes the heads and
+//     the counter, so the next launch on the same block starts clean
 //
 // Windows: up to 64 packets of one segment; descriptors arrive by LDS-DMA into
 // the other half of the wave's double buffer while the current one is swept.
@@ -568,10 +374,13 @@ struct TailArgs {
     unsigned long long* trace;  // diagnostics only (LVLIP_TAIL_TRACE): 8 u64 per streamer, or null
 };
 
-constexpr uint32_t TAIL_MASK = 8u * 32u;  // ctr index of the empty-pool mask
-constexpr uint32_t TAIL_EXIT = 9u * 32u;  // ctr index of the exit counter
-constexpr uint32_t TAIL_WORDS = 10u * 32u;
-constexpr int DYN_THREADS = (SW_WAVES + 1) * 64;
+// Counter words sit 8 KiB apart: atomics on one word serialise at the memory
+// channel that holds it, and words sharing a channel would stall that channel's
+// share of every wave's stream together (measured).
+constexpr uint32_t TAIL_STRIDE = 2048u;             // u32 words between counters
+constexpr uint32_t TAIL_GEXIT = 8u * TAIL_STRIDE;   // 8 exit counters (blockIdx % 8)
+constexpr uint32_t TAIL_FEXIT = 16u * TAIL_STRIDE;  // final exit counter
+constexpr uint32_t TAIL_WORDS = 17u * TAIL_STRIDE;
 constexpr uint32_t TQ = 4;  // queue slots per streamer (one is kept filled)
 
 __device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
@@ -581,120 +390,156 @@ __device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int R, int POL = 0>
-__global__ __launch_bounds__(DYN_THREADS) void k_stream_dyn(const uint8_t* __restrict__ base,
-                                                            const lvlip_csum_desc* __restrict__ descs,
-                                                            uint32_t n, uint32_t per_wave, TailArgs ta,
-                                                            uint16_t* __restrict__ out) {
+// The claimer wave of a DYN workgroup (see above); returns when every streamer
+// of its workgroup has been sent "end".
+__device__ __forceinline__ void tail_claimer(const TailArgs& ta, uint32_t n, uint32_t lane,
+                                             uint32_t (*q_lo)[TQ], uint32_t (*q_hi)[TQ],
+                                             uint32_t* q_tail, const uint32_t* q_head,
+                                             uint32_t* q_end) {
+    auto pool_lo = [&](uint32_t q) { return ta.t0 + q * ta.plen; };
+    auto pool_hi = [&](uint32_t q) {
+        return (uint32_t)min<uint64_t>((uint64_t)ta.t0 + (uint64_t)(q + 1u) * ta.plen, (uint64_t)n);
+    };
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint32_t q = xcc & 7u;          // current pool (uniform)
+    bool all_empty = false;         // every pool used up (uniform)
+    uint32_t pushed = 0;            // lane l < 4: segments pushed to streamer l
+    bool fin = lane >= SW_WAVES;    // lane l < 4: "end" posted to streamer l
+    // The current pool ran dry: read all eight heads (lanes 0-7, plain
+    // system-coherent loads) and move to the pool with the most left, or learn
+    // that none has any.  Atomics on one word serialise at its memory channel
+    // (~87 per us), and a claim on an empty pool is wasted; measured: claimers
+    // probing pools by claiming (and OR-ing an empty mask) slowed the whole
+    // chip's stream by up to 15 %.  Reads do not serialise.
+    auto next_pool = [&]() {
+        uint32_t head = 0xffffffffu;
+        if (lane < 8u) {
+            const uint32_t* hp = ta.ctr + lane * TAIL_STRIDE;
+            asm volatile("global_load_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                         : "=v"(head) : "v"(hp) : "memory");
+        }
+        const uint32_t pl = pool_lo(lane & 7u), ph = pool_hi(lane & 7u);
+        const uint32_t len = ph > pl ? ph - pl : 0u;
+        const uint32_t left = (lane < 8u && head < len) ? len - head : 0u;
+        uint32_t best = 0, bq = q;
+        for (uint32_t l = 0; l < 8u; ++l) {
+            const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)left, (int)l);
+            if (v > best) {
+                best = v;
+                bq = l;
+            }
+        }
+        all_empty = best == 0u;
+        q = bq;
+    };
+    if (pool_hi(q) <= pool_lo(q)) next_pool();  // an empty home pool (tiny tails)
+    for (;;) {
+        const bool need = !fin && pushed - lds_load(&q_head[lane & (SW_WAVES - 1)]) < 1u;
+        const uint64_t needm = __builtin_amdgcn_ballot_w64(need);
+        if (!needm) {
+            if (!__builtin_amdgcn_ballot_w64(!fin)) break;
+            // idle: sleep long (a polling claimer takes issue slots from its
+            // streamers); a streamer's pop wakes it (s_wakeup)
+            __builtin_amdgcn_s_sleep(127);
+            continue;
+        }
+        if (all_empty) {  // nothing left anywhere: post "end"
+            if (!fin) lds_store(&q_end[lane], 1u);
+            fin = true;
+            continue;
+        }
+        const uint32_t m = (uint32_t)__popcll(needm);
+        uint32_t old = 0;
+        if (lane == 0) old = atomicAdd(ta.ctr + q * TAIL_STRIDE, m * ta.chunk);
+        old = uniform(old);
+        const uint32_t pl = pool_lo(q), ph = pool_hi(q);
+        const uint32_t len = ph > pl ? ph - pl : 0u;
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
+        const uint64_t st = (uint64_t)old + (uint64_t)r * ta.chunk;
+        if (need && st < len) {
+            const uint32_t slot = pushed % TQ;
+            lds_store(&q_lo[lane][slot], pl + (uint32_t)st);
+            lds_store(&q_hi[lane][slot], pl + (uint32_t)min<uint64_t>(st + ta.chunk, len));
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // segment before tail
+            lds_store(&q_tail[lane], pushed + 1u);
+            ++pushed;
+        }
+        if ((uint64_t)old + (uint64_t)m * ta.chunk >= len) next_pool();
+    }
+    // exit: the last claimer of each group (blockIdx % 8) counts the group out;
+    // the last group out zeroes every counter for the next launch
+    if (lane == 0) {
+        const uint32_t g = blockIdx.x & 7u;
+        const uint32_t in_g = (ta.nblocks - g + 7u) / 8u;
+        const uint32_t groups = ta.nblocks < 8u ? ta.nblocks : 8u;
+        if (atomicAdd(ta.ctr + TAIL_GEXIT + g * TAIL_STRIDE, 1u) == in_g - 1u &&
+            atomicAdd(ta.ctr + TAIL_FEXIT, 1u) == groups - 1u) {
+            for (uint32_t k = 0; k < 8u; ++k) {
+                atomicExch(ta.ctr + k * TAIL_STRIDE, 0u);
+                atomicExch(ta.ctr + TAIL_GEXIT + k * TAIL_STRIDE, 0u);
+            }
+            atomicExch(ta.ctr + TAIL_FEXIT, 0u);
+        }
+    }
+}
+
+// The ring is organised in pieces: a piece is up to 2 KiB of one packet (two
+// 1 KiB wave-loads, always both issued; chunks past the packet read zeros), so
+// all per-piece bookkeeping is amortised over 2 KiB and a 1500-B segment is one
+// piece.  R pieces are in flight; the oldest is retired by vmcnt(2*(R-1)).
+// (r01 profile of a per-1KiB-slot ring: ~130 SALU per packet, the CU's scalar
+// unit ~80 % busy and the kernel SALU-bound; this layout cuts that ~3x.)
+// DYN: the workgroup is 4 streamers + 1 claimer (tail_claimer above).  A
+// streamer's static segment is [wave*per_wave, ...) up to t0; when its current
+// segment enters its last window it pops the next segment from its LDS queue
+// (the pop's wait is one asm block: a loop in the C++ control flow here would
+// sit inside the ring loop and cost register copies on every packet) and
+// prefetches that segment's first window, so the ring runs on across segment
+// boundaries.  Everything a DYN launch changes sits on the window-entry path;
+// the per-packet path is the static kernel's plus one window-base word per
+// piece (results flush per window, and a window may end with its segment).
+template <int R, int POL = 0, bool DYN = false>
+__global__ __launch_bounds__(DYN ? 320 : 256) void k_stream(const uint8_t* __restrict__ base,
+                                                const lvlip_csum_desc* __restrict__ descs,
+                                                uint32_t n, uint32_t per_wave, TailArgs ta,
+                                                uint16_t* __restrict__ out) {
     __shared__ uint4 s_win[SW_WAVES][2][64];
-    // per streamer: segment ring [lo, hi) x TQ, tail (claimer), head (streamer), end flag
+    // DYN: per streamer, a ring of segments [lo, hi), tail (claimer), head
+    // (streamer), end flag
     __shared__ uint32_t q_lo[SW_WAVES][TQ], q_hi[SW_WAVES][TQ];
     __shared__ uint32_t q_tail[SW_WAVES], q_head[SW_WAVES], q_end[SW_WAVES];
     constexpr uint32_t END = 0xffffffffu;
     constexpr uint32_t PIECE = 2048u;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wid = uniform(threadIdx.x >> 6);
-    if (threadIdx.x < SW_WAVES) {
-        q_tail[threadIdx.x] = 0;
-        q_head[threadIdx.x] = 0;
-        q_end[threadIdx.x] = 0;
-    }
-    __syncthreads();
-
-    auto pool_lo = [&](uint32_t q) { return ta.t0 + q * ta.plen; };
-    auto pool_hi = [&](uint32_t q) {
-        return (uint32_t)min<uint64_t>((uint64_t)ta.t0 + (uint64_t)(q + 1u) * ta.plen, (uint64_t)n);
-    };
-
-    // ------------------------------------------------------------ claimer --
-    if (wid == SW_WAVES) {
-        uint32_t xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        uint32_t q = xcc & 7u, empty = 0;  // current pool, pools known empty (uniform)
-        uint32_t pushed = 0;               // lane l < 4: segments pushed to streamer l
-        bool fin = lane >= SW_WAVES;       // lane l < 4: "end" posted to streamer l
-        for (;;) {
-            const bool need = !fin && pushed - lds_load(&q_head[lane & (SW_WAVES - 1)]) < 1u;
-            const uint64_t needm = __builtin_amdgcn_ballot_w64(need);
-            if (!needm) {
-                if (!__builtin_amdgcn_ballot_w64(!fin)) break;
-                // idle: sleep long (a polling claimer takes issue slots from its
-                // streamers); a streamer's pop wakes it (s_wakeup)
-                __builtin_amdgcn_s_sleep(127);
-                continue;
-            }
-            if (empty == 0xffu) {  // nothing left anywhere: post "end"
-                if (!fin) lds_store(&q_end[lane], 1u);
-                fin = true;
-                continue;
-            }
-            const uint32_t m = (uint32_t)__popcll(needm);
-            uint32_t old = 0;
-            if (lane == 0) old = atomicAdd(ta.ctr + q * 32u, m * ta.chunk);
-            old = uniform(old);
-            const uint32_t pl = pool_lo(q), ph = pool_hi(q);
-            const uint32_t len = ph > pl ? ph - pl : 0u;
-            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
-            const uint64_t st = (uint64_t)old + (uint64_t)r * ta.chunk;
-            if (need && st < len) {
-                const uint32_t slot = pushed % TQ;
-                lds_store(&q_lo[lane][slot], pl + (uint32_t)st);
-                lds_store(&q_hi[lane][slot], pl + (uint32_t)min<uint64_t>(st + ta.chunk, len));
-                __atomic_signal_fence(__ATOMIC_SEQ_CST);  // segment before tail
-                lds_store(&q_tail[lane], pushed + 1u);
-                ++pushed;
-            }
-            if ((uint64_t)old + (uint64_t)m * ta.chunk >= len) {
-                // pool q is used up: tell other claimers, learn what they know
-                uint32_t g = 0;
-                if (lane == 0) {
-                    atomicOr(ta.ctr + TAIL_MASK, 1u << q);
-                    const uint32_t* mp = ta.ctr + TAIL_MASK;
-                    asm volatile("global_load_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
-                                 : "=v"(g) : "v"(mp) : "memory");
-                }
-                empty |= (1u << q) | uniform(g);
-                for (uint32_t t = 1; t <= 8u && (empty >> q) & 1u; ++t) q = (q + 1u) & 7u;
-            }
-        }
-        if (lane == 0 && atomicAdd(ta.ctr + TAIL_EXIT, 1u) == ta.nblocks - 1u) {
-            for (uint32_t k = 0; k < 8u; ++k) atomicExch(ta.ctr + k * 32u, 0u);
-            atomicExch(ta.ctr + TAIL_MASK, 0u);
-            atomicExch(ta.ctr + TAIL_EXIT, 0u);
-        }
-        return;
-    }
-
-    // ---------------------------------------------------------- streamers --
-    // Loop-carried scalars are kept to what every packet needs (ip, io, the
-    // window bounds, the packet's resource words); the segment and next-window
-    // state changes once per window and lives in lanes of one VGPR (ST_*), so
-    // the compiler has no SGPR phis to shuffle on the per-packet path.
-    enum { ST_SEG_HI = 0, ST_X_LO, ST_X_HI, ST_X_SEG_HI, ST_X_VALID, ST_POPPED, ST_WB };
     const uint32_t lane16 = lane * 16u;
+    const uint32_t wid = uniform(threadIdx.x >> 6);
+    if (DYN) {
+        if (threadIdx.x < SW_WAVES) {
+            q_tail[threadIdx.x] = 0;
+            q_head[threadIdx.x] = 0;
+            q_end[threadIdx.x] = 0;
+        }
+        __syncthreads();
+        if (wid == SW_WAVES) {
+            tail_claimer(ta, n, lane, q_lo, q_hi, q_tail, q_head, q_end);
+            return;
+        }
+    }
     const uint32_t wave = uniform(blockIdx.x * SW_WAVES + wid);
-    const unsigned long long t_start = ta.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const uint64_t lo64 = (uint64_t)wave * per_wave;
+    if (lo64 >= n) return;  // never with DYN (launcher: per_wave * waves <= n)
+    uint32_t p_lo = (uint32_t)lo64;
+    uint32_t p_hi = (uint32_t)min<uint64_t>(lo64 + per_wave, DYN ? (uint64_t)min(ta.t0, n) : (uint64_t)n);
+    const unsigned long long t_start = (DYN && ta.trace) ? __builtin_amdgcn_s_memrealtime() : 0ull;
 
-    // static segment (per_wave >= 128 packets: launcher), ends at or before t0
-    const uint32_t s_lo = (uint32_t)min<uint64_t>((uint64_t)wave * per_wave, (uint64_t)n);
-    const uint32_t s_hi = (uint32_t)min<uint64_t>((uint64_t)wave * per_wave + per_wave,
-                                                  (uint64_t)min(ta.t0, n));
-
-    uint32_t st = 0;  // VGPR: lane i = field i
-    auto get = [&](int f) { return (uint32_t)__builtin_amdgcn_readlane((int)st, f); };
-    auto put = [&](int f, uint32_t v) {
-        const uint32_t u = uniform(v);  // LDS-loaded values are not known uniform
-        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(st) : "s"(u), "n"(f));
-    };
-
-    // next segment from the claimer.  The wait for a non-empty queue (or "end")
-    // is one asm block: a loop in the C++ control flow here would sit inside
-    // the ring loop and cost register copies on every packet (measured).
+    // DYN: the next segment, popped when the current one enters its last window
+    uint32_t n_lo = 0, n_hi = 0, popped = 0;
+    bool n_valid = false;
     const uint32_t a_tail = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&q_tail[wid];
     const uint32_t a_end = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&q_end[wid];
-    auto pop = [&](uint32_t& lo, uint32_t& hi) -> bool {
-        const uint32_t popped = get(ST_POPPED);
+    auto pop = [&]() {
         uint32_t vt, ve, tail, fin;
         asm volatile(
             "1:\n\t"
@@ -719,47 +564,32 @@ __global__ __launch_bounds__(DYN_THREADS) void k_stream_dyn(const uint8_t* __res
             // "end" was seen; the claimer writes tail before end, so a fresh
             // read of tail is final
             tail = uniform(lds_load(&q_tail[wid]));
-            if (tail <= popped) return false;
         }
-        const uint32_t slot = popped % TQ;
-        lo = lds_load(&q_lo[wid][slot]);
-        hi = lds_load(&q_hi[wid][slot]);
-        put(ST_POPPED, popped + 1u);
-        lds_store(&q_head[wid], popped + 1u);
-        asm volatile("s_wakeup" ::: "memory");  // the claimer refills the queue
-        return true;
-    };
-
-    // the window after [w_lo, w_hi) -> ST_X_*
-    auto plan_next = [&](uint32_t w_hi) {
-        const uint32_t seg_hi = get(ST_SEG_HI);
-        if (w_hi < seg_hi) {
-            put(ST_X_LO, w_hi);
-            put(ST_X_HI, min(w_hi + 64u, seg_hi));
-            put(ST_X_SEG_HI, seg_hi);
-            put(ST_X_VALID, 1u);
-        } else {
-            uint32_t lo = 0, hi = 0;
-            const bool ok = pop(lo, hi);
-            put(ST_X_LO, lo);
-            put(ST_X_HI, min(lo + 64u, hi));
-            put(ST_X_SEG_HI, hi);
-            put(ST_X_VALID, ok ? 1u : 0u);
+        n_valid = tail > popped;
+        if (n_valid) {
+            const uint32_t slot = popped % TQ;
+            n_lo = uniform(lds_load(&q_lo[wid][slot]));
+            n_hi = uniform(lds_load(&q_hi[wid][slot]));
+            ++popped;
+            lds_store(&q_head[wid], popped);
+            asm volatile("s_wakeup" ::: "memory");  // the claimer refills the queue
         }
     };
 
-    uint32_t w_lo = s_lo, w_hi = min(s_lo + 64u, s_hi);
-    put(ST_SEG_HI, s_hi);
-    put(ST_POPPED, 0u);
-    put(ST_WB, 0u);
-    fetch_window(descs, w_lo, n, lane, s_win[wid][0]);
-    plan_next(w_hi);
-    if (get(ST_X_VALID)) fetch_window(descs, get(ST_X_LO), n, lane, s_win[wid][1]);
+    // descriptor windows: packets [p_lo + 64w, p_lo + 64w + 64) live in
+    // s_win[wid][w & 1] (DYN: the wn-th window of the wave in s_win[wid][wn & 1])
+    uint32_t wn = 0;
+    fetch_window(descs, p_lo, n, lane, s_win[wid][0]);
+    fetch_window(descs, p_lo + 64u, n, lane, s_win[wid][1]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    uint32_t m_x, m_y, m_z, m_t, m_s;
-    auto load_window_meta = [&](uint32_t b) {
-        const uint4 d = s_win[wid][b][lane];
+    // Packet metadata for the issue cursor's window, one packet per lane (VALU,
+    // 64 packets at a time); the issue side pulls its packet's fields with
+    // v_readlane.  (Computing them per packet on the scalar unit made the
+    // kernel SALU-bound: r01 profile.)
+    uint32_t m_x, m_y, m_z, m_t, m_s;  // srd.x, srd.y, srd.z, tinfo, start of packet (window + lane)
+    auto load_window_meta = [&](uint32_t w) {
+        const uint4 d = s_win[wid][w & 1u][lane];
         const PacketMeta pm = packet_meta(base, u32x4{d.x, d.y, d.z, d.w});
         m_x = pm.srd.x;
         m_y = pm.srd.y;
@@ -768,11 +598,21 @@ __global__ __launch_bounds__(DYN_THREADS) void k_stream_dyn(const uint8_t* __res
         m_s = pm.start;
     };
     load_window_meta(0);
+    // DYN, a static segment of one or two windows: the window after it is the
+    // next segment's first (per_wave >= 128 makes this a corner case)
+    if (DYN && p_lo + 64u >= p_hi) {
+        pop();
+        if (n_valid) {
+            fetch_window(descs, n_lo, n, lane, s_win[wid][1]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
 
-    uint32_t ip = w_lo, io = 0;
+    // issue cursor: packet ip (k = ip - p_lo), byte offset io of the next piece in it
+    uint32_t ip = p_lo, io = 0;
     u32x4 srd;
     uint32_t tinfo, start;
-    auto pull = [&](uint32_t k) {
+    auto pull = [&](uint32_t k) {  // k = packet index within its window
         srd.x = (uint32_t)__builtin_amdgcn_readlane((int)m_x, (int)k);
         srd.y = (uint32_t)__builtin_amdgcn_readlane((int)m_y, (int)k);
         srd.z = (uint32_t)__builtin_amdgcn_readlane((int)m_z, (int)k);
@@ -781,64 +621,86 @@ __global__ __launch_bounds__(DYN_THREADS) void k_stream_dyn(const uint8_t* __res
         start = (uint32_t)__builtin_amdgcn_readlane((int)m_s, (int)k);
     };
     pull(0);
-    bool live = true;
 
+    // consume side: raw sums W and seeds of packets [gc, gc+64) gather in lanes
+    uint32_t gc = p_lo;
     uint32_t res_w = 0, res_s = 0;
     uint32_t acc = 0;
-    uint32_t gc = w_lo;  // consume side: first packet of the window being gathered
+
     u32x4 va[R], vb[R];
-    // per piece: packet (END past the work); meta = last | (len & 3) << 1 |
-    // (offset of the last dword in the piece) << 3 | window-last << 14
-    uint32_t s_pkt[R], s_start[R], s_meta[R];
+    // per piece: packet (END past the range), start_sum, and
+    // meta = last | (len & 3) << 1 | (byte offset of the last dword in the piece) << 3
+    // (DYN: that offset masked to 11 bits, bit 14 = the packet ends its segment;
+    // s_wb = first packet of the piece's window)
+    uint32_t s_pkt[R], s_start[R], s_meta[R], s_wb[R];
 
     auto issue = [&](int r) {
+        const bool live = ip < p_hi;  // uniform
         u32x4 sr = srd;
-        if (!live) sr.z = 0;
+        if (!live) sr.z = 0;  // past the range: every dword out of range -> zeros
         const uint32_t off = lane16 + io;
         va[r] = buffer_load_nt_asm<POL>(off, sr);
         vb[r] = buffer_load_nt_asm<POL>(off + 1024u, sr);
+        // srd.z = round_up(len, 4): the piece is the packet's last when it reaches
+        // that (or the packet is empty)
         const bool last = io + PIECE >= srd.z;
-        const bool wlast = last && ip + 1u == w_hi;
         s_pkt[r] = live ? ip : END;
         s_start[r] = start;
-        s_meta[r] = (uint32_t)last | ((tinfo & 3u) << 1) | ((((srd.z - 4u) - io) & 0x7FFu) << 3) |
-                    ((uint32_t)wlast << 14);
+        if (DYN) {
+            s_meta[r] = (uint32_t)last | ((tinfo & 3u) << 1) | ((((srd.z - 4u) - io) & 0x7FFu) << 3) |
+                        ((uint32_t)(last && ip + 1u == p_hi) << 14);
+            s_wb[r] = ip - ((ip - p_lo) & 63u);
+        } else {
+            s_meta[r] = (uint32_t)last | ((tinfo & 3u) << 1) | (((srd.z - 4u) - io) << 3);
+        }
         if (live) {
             if (!last) {
                 io += PIECE;
             } else {
                 ++ip;
                 io = 0;
-                if (ip == w_hi) {  // leaving the window (rare path, one merge point)
-                    if (get(ST_X_VALID)) {
-                        // the next window's DMA was followed by at least one
-                        // piece (two loads): vmcnt(2) retires it (issue order)
-                        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                        const uint32_t wb = get(ST_WB) ^ 1u;
-                        put(ST_WB, wb);
-                        w_lo = get(ST_X_LO);
-                        w_hi = get(ST_X_HI);
-                        put(ST_SEG_HI, get(ST_X_SEG_HI));
-                        load_window_meta(wb);
-                        ip = w_lo;
-                        plan_next(w_hi);
-                        if (get(ST_X_VALID)) fetch_window(descs, get(ST_X_LO), n, lane, s_win[wid][wb ^ 1u]);
-                    } else {
-                        live = false;
-                    }
+                if (DYN && ip == p_hi && n_valid) {  // on to the next segment
+                    p_lo = n_lo;
+                    p_hi = n_hi;
+                    ip = p_lo;
+                    n_valid = false;
                 }
-                if (live) pull(ip - w_lo);
+                if (ip < p_hi) {
+                    const uint32_t k = ip - p_lo;
+                    if ((k & 63u) == 0u) {  // entered window k/64
+                        if (DYN) {
+                            // a short window's DMA may be only one piece old:
+                            // retire it (vector-memory ops retire in issue order)
+                            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                            ++wn;
+                            load_window_meta(wn);
+                            if (ip + 64u < p_hi) {
+                                fetch_window(descs, ip + 64u, n, lane, s_win[wid][(wn + 1u) & 1u]);
+                            } else {
+                                pop();
+                                if (n_valid) fetch_window(descs, n_lo, n, lane, s_win[wid][(wn + 1u) & 1u]);
+                            }
+                        } else {
+                            load_window_meta(k >> 6);
+                            fetch_window(descs, ip + 64u, n, lane, s_win[wid][((k >> 6) + 1u) & 1u]);
+                        }
+                    }
+                    pull(k & 63u);
+                }
             }
         }
     };
 
     auto consume = [&](int r) {
+        // Piece r's two loads are the oldest in flight: 2*(R-1) ring loads (and
+        // possibly result stores / window DMAs, which only make this stricter)
+        // were issued after them.
         piece_wait<2 * (R - 1)>(va[r], vb[r]);
         u32x4 x = va[r], y = vb[r];
         const uint32_t meta = s_meta[r];
         const uint32_t len3 = (meta >> 1) & 3u;
-        if ((meta & 1u) && len3) {
-            const uint32_t pos = (meta >> 3) & 0x7FFu;
+        if ((meta & 1u) && len3) {  // uniform: keep bytes [0, len & 3) of the last dword
+            const uint32_t pos = DYN ? (meta >> 3) & 0x7FFu : meta >> 3;  // byte offset of that dword in the piece
             const uint32_t m = (1u << (8u * len3)) - 1u;
             const bool me = lane == ((pos >> 4) & 63u);
             const uint32_t tk = (pos >> 2) & 3u;
@@ -862,17 +724,19 @@ __global__ __launch_bounds__(DYN_THREADS) void k_stream_dyn(const uint8_t* __res
         if (meta & 1u) {
             const uint32_t w = wave_sum_dpp(acc);
             acc = 0;
-            const uint32_t k = s_pkt[r] - gc;
+            const uint32_t g0 = DYN ? s_wb[r] : gc;
+            const uint32_t k = s_pkt[r] - g0;
             if (lane == k) {
                 res_w = w;
                 res_s = s_start[r];
             }
-            if (meta & (1u << 14)) {
+            if (k == 63u || (DYN ? (meta >> 14) & 1u : s_pkt[r] + 1u == p_hi)) {
+                // fold 64 results at once (src/utils.c:46-54, per lane)
                 uint32_t tt = res_s + res_w;
                 tt = (tt & 0xffffu) + (tt >> 16);
                 tt = (tt & 0xffffu) + (tt >> 16);
-                if (lane <= k) out[gc + lane] = (uint16_t)~tt;
-                gc = END;  // the next window's first packet sets it
+                if (lane <= k) out[g0 + lane] = (uint16_t)~tt;
+                gc += 64u;
             }
         }
     };
@@ -887,24 +751,22 @@ __global__ __launch_bounds__(DYN_THREADS) void k_stream_dyn(const uint8_t* __res
                 done = true;
                 break;
             }
-            if (gc == END) gc = s_pkt[r];  // first piece of a new window
             consume(r);
             issue(r);
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (ta.trace && lane == 0) {
-        uint32_t xid;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this wave left in flight
+    if (DYN && ta.trace && lane == 0) {
+        uint32_t xid, hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xid));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         unsigned long long* t = ta.trace + (uint64_t)wave * 8u;
         t[0] = t_start;
         t[1] = 0;
         t[2] = __builtin_amdgcn_s_memrealtime();
-        uint32_t hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        t[3] = get(ST_POPPED);
+        t[3] = popped;
         t[4] = xid & 7u;
-        t[5] = s_hi - s_lo;
+        t[5] = per_wave;
         t[6] = wid;
         t[7] = hw;
     }
@@ -1478,34 +1340,25 @@ void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvli
     waves = (waves + 3) & ~3ull;  // whole 256-thread blocks
     const uint32_t per_wave = (uint32_t)(((uint64_t)n + waves - 1) / waves);
     const uint32_t grid = (uint32_t)(waves / 4);
+    lvlip::TailArgs ta{};  // static split: no counter block
     switch (load_policy()) {
 #define LVLIP_STREAM_POL(P)                                                              \
     case P:                                                                              \
         hipLaunchKernelGGL((lvlip::k_stream<U, P>), dim3(grid), dim3(256), 0, s,         \
-                           (const uint8_t*)base, d, n, per_wave, out);                   \
+                           (const uint8_t*)base, d, n, per_wave, ta, out);               \
         break;
         LVLIP_STREAM_POL(1)
         LVLIP_STREAM_POL(2)
         LVLIP_STREAM_POL(3)
         LVLIP_STREAM_POL(4)
 #undef LVLIP_STREAM_POL
-        default: {
-            static const bool sleeper = getenv("LVLIP_STREAM_SLEEPER") != nullptr;  // diagnostic
-            static const bool pad = getenv("LVLIP_STREAM_PAD") != nullptr;          // diagnostic
-            if (pad)
-                hipLaunchKernelGGL((lvlip::k_stream<U, 0, false, 16>), dim3(grid), dim3(256), 0, s,
-                                   (const uint8_t*)base, d, n, per_wave, out);
-            else if (sleeper)
-                hipLaunchKernelGGL((lvlip::k_stream<U, 0, true>), dim3(grid), dim3(320), 0, s,
-                                   (const uint8_t*)base, d, n, per_wave, out);
-            else
-                hipLaunchKernelGGL((lvlip::k_stream<U, 0>), dim3(grid), dim3(256), 0, s,
-                                   (const uint8_t*)base, d, n, per_wave, out);
-        }
+        default:
+            hipLaunchKernelGGL((lvlip::k_stream<U, 0>), dim3(grid), dim3(256), 0, s,
+                               (const uint8_t*)base, d, n, per_wave, ta, out);
     }
 }
 
-// ---- dynamic tail of the stream kernel (k_stream_dyn) ----
+// ---- dynamic tail of the stream kernel (k_stream<.., DYN = true>) ----
 //
 // Counter blocks: one per (device, stream), from a per-device pool allocated
 // and zeroed once.  Launches on one stream are serialised, so they may share a
@@ -1515,7 +1368,7 @@ void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvli
 // kernel that owns scratch).  When no block is available (pool exhausted, the
 // per-thread default stream, first use while capturing) the launch uses the
 // static split.
-constexpr int kTailSlots = 256;
+constexpr int kTailSlots = 64;  // 139 KiB each
 
 struct TailPool {
     uint32_t* mem = nullptr;
@@ -1615,13 +1468,13 @@ bool launch_stream_dyn(int waves_per_cu, hipStream_t s, const void* base,
     switch (load_policy()) {
 #define LVLIP_DYN_POL(P)                                                                 \
     case P:                                                                              \
-        hipLaunchKernelGGL((lvlip::k_stream_dyn<U, P>), dim3(grid), dim3(lvlip::DYN_THREADS), 0, s, \
+        hipLaunchKernelGGL((lvlip::k_stream<U, P, true>), dim3(grid), dim3(320), 0, s,   \
                            (const uint8_t*)base, d, n, pw, ta, out);                     \
         break;
         LVLIP_DYN_POL(1)
 #undef LVLIP_DYN_POL
         default:
-            hipLaunchKernelGGL((lvlip::k_stream_dyn<U, 0>), dim3(grid), dim3(lvlip::DYN_THREADS), 0, s,
+            hipLaunchKernelGGL((lvlip::k_stream<U, 0, true>), dim3(grid), dim3(320), 0, s,
                                (const uint8_t*)base, d, n, pw, ta, out);
     }
     return true;
@@ -1689,7 +1542,7 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         case LVLIP_KERNEL_WAVE_DYN: {
             // unroll = 2-KiB pieces in flight per wave (2 = up to 4 KiB).
             // WAVE_STATIC: static split (k_stream); WAVE_DYN: dynamic tail
-            // (k_stream_dyn) where it applies; WAVE: static unless
+            // (k_stream<.., DYN>) where it applies; WAVE: static unless
             // LVLIP_TAIL_PCT > 0 (DESIGN.md §8 has the measurements).
             if (unroll <= 0) unroll = 2;
             const int w = wpc > 0 ? wpc : 16;

@@ -55,11 +55,16 @@ def functions(text):
     return funcs
 
 
+def is_dyn(name):
+    """k_stream<R, POL, DYN = true> (mangled ...ELb1E...)."""
+    return "ELb1E" in name
+
+
 def stream_kernels(asm):
     f = functions(asm)
     ks = {n: body for n, body in f.items() if "k_stream" in n}
     assert ks, "no k_stream instantiations found"
-    assert any("k_stream_dyn" in n for n in ks), "no k_stream_dyn instantiations found"
+    assert any(is_dyn(n) for n in ks), "no k_stream<.., DYN = true> instantiations found"
     return ks
 
 
@@ -90,8 +95,8 @@ def test_lds_dma_m0_sequence(asm):
 
 def test_ring_waits_are_counted_not_draining(asm):
     for name, body in stream_kernels(asm).items():
-        if "k_stream_dyn" in name:
-            continue  # test_dyn_waits_and_claims
+        if is_dyn(name):
+            continue  # test_dyn_streamers_never_drain
         r = int(re.search(r"k_streamILi(\d+)E", name).group(1))  # pieces in flight
         waits = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt" in ins]
         ring = [w for w in waits if f"vmcnt({2 * (r - 1)})" in w]
@@ -108,14 +113,14 @@ def test_no_scratch(asm):
 
 
 def test_dyn_streamers_never_drain(asm):
-    """k_stream_dyn: the streamers keep k_stream's counted ring waits; the only
-    draining waits are the first window fill, the streamer exit and the
+    """k_stream with DYN: the streamers keep the counted ring waits; the only
+    draining waits are the first window fill(s), the streamer exit and the
     claimer's own waits on its atomics (a global atomic or the sc0 sc1 mask
     read shortly before).  No AGPRs."""
     for name, body in stream_kernels(asm).items():
-        if "k_stream_dyn" not in name:
+        if not is_dyn(name):
             continue
-        r = int(re.search(r"k_stream_dynILi(\d+)E", name).group(1))
+        r = int(re.search(r"k_streamILi(\d+)E", name).group(1))
         waits = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt" in ins]
         assert sum(f"vmcnt({2 * (r - 1)})" in w for w in waits) >= r, (name, waits)
         other = 0
@@ -126,5 +131,5 @@ def test_dyn_streamers_never_drain(asm):
                               (x.startswith("global_load_dword") and "sc0 sc1" in x) for x in near)
                 if not claimer:
                     other += 1
-        assert other <= 3, (name, other)
+        assert other <= 4, (name, other)
         assert not any(re.search(r"\ba\[?\d+", ins) for ins in body), name
