@@ -372,6 +372,7 @@ struct TailArgs {
     uint32_t chunk;   // packets per claim
     uint32_t nblocks; // workgroups in the grid
     unsigned long long* trace;  // diagnostics only (LVLIP_TAIL_TRACE): 8 u64 per streamer, or null
+    uint32_t epoch;   // FB: launch number on this counter block (host-counted, >= 1)
 };
 
 // Counter words sit 8 KiB apart: atomics on one word serialise at the memory
@@ -382,6 +383,94 @@ constexpr uint32_t TAIL_GEXIT = 8u * TAIL_STRIDE;   // 8 exit counters (blockIdx
 constexpr uint32_t TAIL_FEXIT = 16u * TAIL_STRIDE;  // final exit counter
 constexpr uint32_t TAIL_WORDS = 17u * TAIL_STRIDE;
 constexpr uint32_t TQ = 4;  // queue slots per streamer (one is kept filled)
+
+// ------------------------------ slot weights from the last launch (FB = true) --
+//
+// Blocks are dealt round-robin over the XCDs and the mapping blockIdx % 8 ->
+// XCD is the same from launch to launch, and so is each XCD's streaming rate
+// (scripts/lab_placement.py: 12 launches, every block on XCD b % 8; per-slot
+// end times stable to a few us, 200-251 us apart at 16 waves/CU).  So an FB
+// launch gives slot s = blockIdx % 8 a share W_s of the batch, set from the
+// previous launch on the same counter block: W_s' ∝ W_s / duration_s (half way
+// there per launch, each within 3/4..5/4 of even), and every wave of the slot
+// an equal part of it.  The partition is a pure function of (n, grid, W), and
+// every wave reads the same W and durations (system-coherent loads of values
+// only the previous launch wrote), so the packets are covered exactly once
+// whatever the weights or placement; placement only decides whether it pays.
+// Per launch e: read W[(e-1)&1], D[(e-1)&1]; block 0 writes W[e&1]; each block
+// atomicMax-es (e << 32 | its longest wave duration) into D[e&1][slot].
+constexpr uint32_t FB_TOTAL = 1u << 24;             // weights' fixed-point sum
+static_assert(SW_WAVES == 4, "FB splits a slot's stripe share with >> 2");
+constexpr uint32_t FB_W = 64u;                      // W[2][8] u32 at words 64..79
+__device__ __forceinline__ uint32_t fb_d_word(uint32_t slot, uint32_t par) {
+    return (1u + slot) * TAIL_STRIDE + 16u + 2u * par;  // u64, 8 KiB apart per slot
+}
+
+// This launch's weights (identical in every wave).  Lanes 0-7 fetch W[s] and
+// D[s] of the previous launch in one round trip (two system-coherent vector
+// loads, one wait); the wave then reads them out lane by lane.
+__device__ __forceinline__ void fb_weights(const TailArgs& ta, uint32_t* w) {
+    const uint32_t pe = (ta.epoch - 1u) & 1u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l8 = lane & 7u;
+    const uint32_t* wa = ta.ctr + FB_W + pe * 8u + l8;
+    const uint32_t* da = ta.ctr + fb_d_word(l8, pe);
+    uint32_t wv;
+    uint64_t dv;
+    asm volatile(
+        "global_load_dword %0, %2, off sc0 sc1\n\t"
+        "global_load_dwordx2 %1, %3, off sc0 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(wv), "=&v"(dv)
+        : "v"(wa), "v"(da)
+        : "memory");
+    uint32_t wp[8];
+    uint64_t dur[8];
+    uint64_t wsum = 0;
+    bool ok = true;
+#pragma unroll
+    for (uint32_t s = 0; s < 8u; ++s) {
+        wp[s] = (uint32_t)__builtin_amdgcn_readlane((int)wv, (int)s);
+        const uint32_t dlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dv, (int)s);
+        const uint32_t dhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(dv >> 32), (int)s);
+        dur[s] = dlo;
+        ok = ok && dhi == ta.epoch - 1u && dlo != 0u;
+        wsum += wp[s];
+    }
+    ok = ok && wsum == FB_TOTAL;
+    constexpr uint32_t EVEN = FB_TOTAL / 8u;
+    if (!ok) {
+#pragma unroll
+        for (uint32_t s = 0; s < 8u; ++s) w[s] = EVEN;
+        return;
+    }
+    // IEEE double (exact for these magnitudes' products, correctly rounded
+    // quotients): every wave computes the same bits, and it avoids the
+    // software 64-bit integer divisions (~24 of them cost each wave ~8 us at
+    // start, measured)
+    double rate[8], rsum = 0.0;
+#pragma unroll
+    for (uint32_t s = 0; s < 8u; ++s) {
+        rate[s] = (double)wp[s] / (double)dur[s];
+        rsum += rate[s];
+    }
+    double v[8], vsum = 0.0;
+#pragma unroll
+    for (uint32_t s = 0; s < 8u; ++s) {
+        const double target = (double)FB_TOTAL * rate[s] / rsum;
+        double x = 0.5 * ((double)wp[s] + target);
+        x = x < 0.75 * EVEN ? 0.75 * EVEN : (x > 1.25 * EVEN ? 1.25 * EVEN : x);
+        v[s] = x;
+        vsum += x;
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < 7u; ++s) {
+        w[s] = (uint32_t)(v[s] * (double)FB_TOTAL / vsum);
+        acc += w[s];
+    }
+    w[7] = FB_TOTAL - acc;
+}
 
 __device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -500,7 +589,7 @@ __device__ __forceinline__ void tail_claimer(const TailArgs& ta, uint32_t n, uin
 // boundaries.  Everything a DYN launch changes sits on the window-entry path;
 // the per-packet path is the static kernel's plus one window-base word per
 // piece (results flush per window, and a window may end with its segment).
-template <int R, int POL = 0, bool DYN = false>
+template <int R, int POL = 0, bool DYN = false, bool FB = false>
 __global__ __launch_bounds__(DYN ? 320 : 256) void k_stream(const uint8_t* __restrict__ base,
                                                 const lvlip_csum_desc* __restrict__ descs,
                                                 uint32_t n, uint32_t per_wave, TailArgs ta,
@@ -528,11 +617,53 @@ __global__ __launch_bounds__(DYN ? 320 : 256) void k_stream(const uint8_t* __res
         }
     }
     const uint32_t wave = uniform(blockIdx.x * SW_WAVES + wid);
-    const uint64_t lo64 = (uint64_t)wave * per_wave;
-    if (lo64 >= n) return;  // never with DYN (launcher: per_wave * waves <= n)
-    uint32_t p_lo = (uint32_t)lo64;
-    uint32_t p_hi = (uint32_t)min<uint64_t>(lo64 + per_wave, DYN ? (uint64_t)min(ta.t0, n) : (uint64_t)n);
-    const unsigned long long t_start = (DYN && ta.trace) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long t_start =
+        (FB || (DYN && ta.trace)) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    __shared__ uint32_t fb_dmax, fb_cnt;
+    uint32_t p_lo, p_hi, fb_w_slot = 0;
+    if (FB) {
+        if (threadIdx.x == 0) {
+            fb_dmax = 0;
+            fb_cnt = 0;
+        }
+        uint32_t w[8];
+        fb_weights(ta, w);
+        const uint32_t slot = blockIdx.x & 7u;
+        fb_w_slot = w[slot];
+        if (blockIdx.x == 0 && wid == 0 && lane == 0) {  // next launch's input
+            uint32_t* wn = ta.ctr + FB_W + (ta.epoch & 1u) * 8u;
+#pragma unroll
+            for (uint32_t s = 0; s < 8u; ++s)
+                asm volatile("global_store_dword %0, %1, off sc0 sc1" :: "v"(wn + s), "v"(w[s]) : "memory");
+        }
+        // Stripes keep the static kernel's interleaving (every XCD reads the
+        // whole buffer; one contiguous region per XCD measured slower): stripe
+        // k = blockIdx / 8 covers [n*k/K, n*(k+1)/K), K = grid / 8, and slot s
+        // takes its W_s share of every stripe, split evenly over its 4 waves.
+        const uint32_t K = ta.nblocks >> 3;  // launcher: grid % 8 == 0
+        const uint32_t k = blockIdx.x >> 3;
+        // n*k < 2^45 is exact in double, and a quotient of integers below
+        // 2^53 that is not an integer lies at least 2^-45 (relative) from one,
+        // so the correctly rounded quotient floors to the integer quotient;
+        // every wave computes the same bits
+        const uint64_t S = (uint64_t)((double)n * (double)k / (double)K);
+        const uint64_t E = (uint64_t)((double)n * (double)(k + 1u) / (double)K);
+        const uint64_t L = E - S;
+        uint64_t c0 = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < 8u; ++s) c0 += s < slot ? w[s] : 0u;
+        const uint64_t a0 = S + ((L * c0) >> 24);                 // FB_TOTAL = 2^24
+        const uint64_t b0 = S + ((L * (c0 + w[slot])) >> 24);
+        const uint64_t part = b0 - a0;
+        p_lo = (uint32_t)(a0 + ((part * wid) >> 2));                // SW_WAVES = 4
+        p_hi = (uint32_t)(a0 + ((part * (wid + 1u)) >> 2));
+        __syncthreads();  // fb_dmax / fb_cnt initialised before any wave's exit
+    } else {
+        const uint64_t lo64 = (uint64_t)wave * per_wave;
+        if (lo64 >= n) return;  // never with DYN (launcher: per_wave * waves <= n)
+        p_lo = (uint32_t)lo64;
+        p_hi = (uint32_t)min<uint64_t>(lo64 + per_wave, DYN ? (uint64_t)min(ta.t0, n) : (uint64_t)n);
+    }
 
     // DYN: the next segment, popped when the current one enters its last window
     uint32_t n_lo = 0, n_hi = 0, popped = 0;
@@ -756,6 +887,21 @@ __global__ __launch_bounds__(DYN ? 320 : 256) void k_stream(const uint8_t* __res
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this wave left in flight
+    if (FB && lane == 0) {
+        // the block's longest wave, into D[e & 1][slot] for the next launch
+        const uint32_t d = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
+        __hip_atomic_fetch_max(&fb_dmax, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__hip_atomic_fetch_add(&fb_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+            SW_WAVES - 1u) {
+            const uint32_t dm = __hip_atomic_load(&fb_dmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            atomicMax(reinterpret_cast<unsigned long long*>(ta.ctr + fb_d_word(blockIdx.x & 7u, ta.epoch & 1u)),
+                      ((unsigned long long)ta.epoch << 32) | (dm ? dm : 1u));
+            if (ta.trace) {  // diagnostics: {duration, slot's weight, slot, epoch} per block
+                ta.trace[blockIdx.x * 2u] = ((unsigned long long)fb_w_slot << 32) | dm;
+                ta.trace[blockIdx.x * 2u + 1u] = ((unsigned long long)ta.epoch << 32) | (blockIdx.x & 7u);
+            }
+        }
+    }
     if (DYN && ta.trace && lane == 0) {
         uint32_t xid, hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xid));
@@ -1331,8 +1477,15 @@ bool flat_contig() {
 }
 
 template <int U>
+bool launch_stream_fb(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                      uint32_t n, uint32_t per_wave, uint16_t* out);
+
+// fb: weight the eight blockIdx % 8 slots by the last launch's timing (FB, see
+// fb_weights; LVLIP_STREAM_FB=1); falls back to the plain static split when it
+// does not apply.
+template <int U>
 void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
-                   uint32_t n, uint16_t* out) {
+                   uint32_t n, uint16_t* out, bool fb = false) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     uint64_t waves = (uint64_t)cu_count(dev) * (uint64_t)waves_per_cu;
@@ -1341,6 +1494,7 @@ void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvli
     const uint32_t per_wave = (uint32_t)(((uint64_t)n + waves - 1) / waves);
     const uint32_t grid = (uint32_t)(waves / 4);
     lvlip::TailArgs ta{};  // static split: no counter block
+    if (fb && launch_stream_fb<U>(grid, s, base, d, n, per_wave, out)) return;
     switch (load_policy()) {
 #define LVLIP_STREAM_POL(P)                                                              \
     case P:                                                                              \
@@ -1375,11 +1529,13 @@ struct TailPool {
     bool failed = false;
     int used = 0;
     std::vector<std::pair<uintptr_t, int>> by_stream;
+    uint32_t epoch[kTailSlots] = {};  // FB launches so far, per block
 };
 std::mutex g_tail_mu;
 TailPool g_tail[64];
 
-uint32_t* tail_block(int dev, hipStream_t s) {
+// epoch (optional): incremented for the block and returned (FB launches).
+uint32_t* tail_block(int dev, hipStream_t s, uint32_t* epoch = nullptr) {
     if (dev < 0 || dev >= 64 || s == hipStreamPerThread) return nullptr;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) != hipSuccess) return nullptr;
@@ -1399,13 +1555,53 @@ uint32_t* tail_block(int dev, hipStream_t s) {
         }
         p.mem = (uint32_t*)m;
     }
+    int slot = -1;
     if (!capturing)
         for (const auto& e : p.by_stream)
-            if (e.first == (uintptr_t)s) return p.mem + (size_t)e.second * lvlip::TAIL_WORDS;
-    if (p.used >= kTailSlots) return nullptr;
-    const int slot = p.used++;
-    if (!capturing) p.by_stream.emplace_back((uintptr_t)s, slot);
+            if (e.first == (uintptr_t)s) slot = e.second;
+    if (slot < 0) {
+        if (p.used >= kTailSlots) return nullptr;
+        slot = p.used++;
+        if (!capturing) p.by_stream.emplace_back((uintptr_t)s, slot);
+    }
+    if (epoch) {
+        if (++p.epoch[slot] == 0) p.epoch[slot] = 1;  // 0 is "never launched"
+        *epoch = p.epoch[slot];
+    }
     return p.mem + (size_t)slot * lvlip::TAIL_WORDS;
+}
+
+// LVLIP_STREAM_FB=1 turns the slot weights on (A/B, off by default: k_stream's
+// slots already end within ~3 % of each other); read once.
+bool fb_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("LVLIP_STREAM_FB");
+        return e && strcmp(e, "1") == 0;
+    }();
+    return v;
+}
+
+template <int U>
+bool launch_stream_fb(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                      uint32_t n, uint32_t per_wave, uint16_t* out) {
+    // every slot needs blocks, and enough packets per wave to be worth it
+    if (grid < 8u || (grid & 7u) || per_wave < 64u || load_policy() != 0) return false;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    lvlip::TailArgs ta{};
+    ta.ctr = tail_block(dev, s, &ta.epoch);
+    if (!ta.ctr) return false;
+    static const bool freeze = getenv("LVLIP_FB_FREEZE") != nullptr;  // diagnostic: even weights
+    if (freeze) ta.epoch = 1;
+    static unsigned long long* const trace = [] {
+        const char* e = getenv("LVLIP_FB_TRACE");  // device address (diagnostics)
+        return e ? (unsigned long long*)(uintptr_t)strtoull(e, nullptr, 0) : nullptr;
+    }();
+    ta.trace = trace;
+    ta.nblocks = grid;
+    hipLaunchKernelGGL((lvlip::k_stream<U, 0, false, true>), dim3(grid), dim3(256), 0, s,
+                       (const uint8_t*)base, d, n, per_wave, ta, out);
+    return true;
 }
 
 // LVLIP_TAIL_PCT: share of the batch left to claims (default 0 = static split,
@@ -1549,18 +1745,19 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             const bool dyn = kernel != LVLIP_KERNEL_WAVE_STATIC;
             const bool xd = kernel == LVLIP_KERNEL_WAVE_DYN;
             const int hint = cfg ? cfg->len_hint : 0;
+            const bool fb = kernel == LVLIP_KERNEL_WAVE && fb_enabled();
             switch (unroll) {
                 case 2:
                     if (!dyn || !launch_stream_dyn<2>(w, s, base, descs, n, out, hint, xd))
-                        launch_stream<2>(w, s, base, descs, n, out);
+                        launch_stream<2>(w, s, base, descs, n, out, fb);
                     break;
                 case 3:
                     if (!dyn || !launch_stream_dyn<3>(w, s, base, descs, n, out, hint, xd))
-                        launch_stream<3>(w, s, base, descs, n, out);
+                        launch_stream<3>(w, s, base, descs, n, out, fb);
                     break;
                 case 4:
                     if (!dyn || !launch_stream_dyn<4>(w, s, base, descs, n, out, hint, xd))
-                        launch_stream<4>(w, s, base, descs, n, out);
+                        launch_stream<4>(w, s, base, descs, n, out, fb);
                     break;
                 default: return LVLIP_EINVAL;
             }

@@ -28,6 +28,8 @@ def main():
     sink = torch.zeros(1, dtype=torch.int32, device=dev)
     ctr = torch.zeros(8 * 32, dtype=torch.int32, device=dev)
     variants = [(0, 8, 0, 2), (0, 4, 0, 4)]
+    if os.environ.get("TL_BPC"):  # oversubscribed static grids: blocks per CU
+        variants = [(0, 8, 0, int(b)) for b in os.environ["TL_BPC"].split(",")]
     if os.environ.get("TL_DYN"):
         for gp in (16, 64):
             variants.append((1, 8, gp, 2))
@@ -83,6 +85,7 @@ def main():
             r["claims_max"] = int(a[:, 3].max())
             r["per_xcc_end_pct_us"] = per_xcc_pct
             r["n_waves_per_xcc"] = {int(x): int(np.sum(xcc == x)) for x in range(8)}
+            r["xcc_busy_end_us"] = {int(x): float(np.max(en[xcc == x])) for x in range(8) if np.any(xcc == x)}
             print(f"{key:34s} {r['GBps_med']:7.1f} GB/s  start p50/p99/max "
                   f"{r['start_us'][0]:.2f}/{r['start_us'][1]:.2f}/{r['start_us'][2]:.2f} us  "
                   f"end p0/p10/p50/p90/p99/max " + "/".join(f"{x:.1f}" for x in r["end_us"]) +

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of the stream kernel's schedule (diagnostic): WAVE (static segments +
-dynamic tail, k_stream_dyn) against WAVE_STATIC (k_stream), interleaved rounds
+"""A/B of the stream kernel's schedule (diagnostic): by default WAVE_DYN
+(static segments + dynamic tail) against WAVE_STATIC; AB_KERNELS picks others
+(e.g. wave,wave_static: slot weights from the last launch vs none), interleaved rounds
 on one resident batch, each launch timed alone with HIP events on its stream.
 The tail knobs are environment variables read once per process
 (LVLIP_TAIL_PCT, LVLIP_TAIL_CHUNK), so sweep them with one process each.
@@ -24,7 +25,8 @@ def main():
     base, descs, out = workloads.to_device(b)
     hint = b.algo_bytes // b.n
     s = torch.cuda.current_stream()
-    variants = {"dyn": lvlip.KERNEL_WAVE_DYN, "static": lvlip.KERNEL_WAVE_STATIC}
+    names = os.environ.get("AB_KERNELS", "wave_dyn,wave_static").split(",")
+    variants = {k: lvlip.KERNEL_NAMES[k] for k in names}
     res = {k: [] for k in variants}
     for _ in range(3):
         for name, k in variants.items():

@@ -446,6 +446,53 @@ def test_stream_dynamic_tail(name, n, hint):
     del g
 
 
+@pytest.mark.parametrize("name,n", [("tcp1500", 300000), ("tcp9000", 100000), ("mixed", 150000)])
+def test_stream_slot_weights_relaunch(name, n):
+    """The slot weights (FB, LVLIP_STREAM_FB=1 in a child process: the knob is
+    read once per process) change from launch to launch on one stream (and
+    start over on a new stream): every launch must stay bit-exact, and so must
+    a graph replay and a second stream running at the same time."""
+    import subprocess
+    import sys
+    if os.environ.get("LVLIP_STREAM_FB") != "1":
+        env = dict(os.environ, LVLIP_STREAM_FB="1")
+        r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                            f"{__file__}::test_stream_slot_weights_relaunch[{name}-{n}]"],
+                           env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+        return
+    b = workloads.make(name, n=n)
+    base, descs, out = workloads.to_device(b)
+    hint = b.algo_bytes // b.n
+    want = pyoracle.batch(base.cpu().numpy(), b.descs, threads=THREADS)
+    for rep in range(12):
+        out.fill_(0)
+        lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_WAVE, len_hint=hint)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint16)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (rep, bad.size, bad[:5])
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.zeros_like(out) for _ in range(6)]
+    for i, o in enumerate(outs):
+        st = s1 if i % 2 == 0 else s2
+        with torch.cuda.stream(st):
+            lvlip.batch_torch(base, descs, o, kernel=lvlip.KERNEL_WAVE, stream=st, len_hint=hint)
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy().view(np.uint16), want), i
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_WAVE,
+                          stream=torch.cuda.current_stream(), len_hint=hint)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    del g
+
+
 def test_max_int_packet():
     """The reference's `int count` at its maximum: one packet of INT_MAX bytes
     (odd length, odd offset, u32 word sum wrapping ~16 times), plus a 1 GiB
