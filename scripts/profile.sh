@@ -10,7 +10,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${OUT:-gpurun_out/prof}
 mkdir -p $OUT
 BENCH=${BENCH:-"bench.py --steps 20 --warmup 3 --no-cpu-baseline"}
 KRE=${KRE:-k_stream}
