@@ -43,7 +43,9 @@
 #include <mutex>
 #include <vector>
 
+#include "flat_src.h"
 #include "lvlip_csum.h"
+#include "lvlip_skb.h"
 
 namespace lvlip {
 
@@ -1182,10 +1184,9 @@ __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
     return ((1u << w) - 1u) << (8 * s);
 }
 
-template <int U, bool NT = true, bool CONTIG = true>
-__global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
-                                              const lvlip_csum_desc* __restrict__ descs,
-                                              uint32_t n, uint16_t* __restrict__ out) {
+template <int U, bool NT, bool CONTIG, class Src>
+__global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, const Src src,
+                                              uint32_t n) {
     __shared__ uint4 s_rec[FT];        // by rank: {a0 lo, a0 hi, cstart, meta}
     __shared__ uint2 s_grp[FGROUPS];   // by 64-chunk group: head bitmap {lo, hi}
     __shared__ uint16_t s_hb[FGROUPS]; // by 64-chunk group: heads before it (<= FT)
@@ -1200,11 +1201,11 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
     const uint32_t i_me = tile0 + t;
 
     // ---- phase 1: descriptors -> chunk counts, ranks, records, head bitmap
-    uint32_t start_sum = 0, nch = 0, meta = 0, lo = 0, lastv = 16;
+    uint32_t start_sum = 0, nch = 0, meta = 0, lo = 0, lastv = 16, ctx = 0;
     uint64_t a0 = 0;
     bool big = false;
     if (i_me < n) {
-        const lvlip_csum_desc d = descs[i_me];
+        const lvlip_csum_desc d = src.get(i_me, ctx);
         start_sum = d.start_sum;
         if (d.len > 0) {
             const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
@@ -1347,7 +1348,8 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
     // ---- phase 3: packets longer than FCAP chunks, one wave each
     for (uint32_t q = wid; q < nbig; q += 4u) {
         const uint32_t tq = s_big[q];
-        const lvlip_csum_desc d = descs[tile0 + tq];
+        uint32_t cq;
+        const lvlip_csum_desc d = src.get(tile0 + tq, cq);
         const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
         const int lo = (int)(abs & 15ull);
         const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
@@ -1365,6 +1367,7 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
     // The sweep summed whole 16-B chunks; subtract, once per packet, the bytes
     // of its first and last chunk that lie outside it (same parity convention,
     // mod 2^32 — exact).
+    uint16_t res = 0;
     if (i_me < n) {
         uint32_t acc = s_acc[t];
         if (meta & (3u << 10)) {
@@ -1389,8 +1392,9 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base,
             }
             acc -= c;
         }
-        out[i_me] = finish(start_sum, acc);
+        res = finish(start_sum, acc);
     }
+    src.put(i_me, res, ctx, i_me < n);
 }
 }  // namespace lvlip
 
@@ -1793,8 +1797,9 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             switch (unroll * 4 + (nt ? 2 : 0) + (contig ? 1 : 0)) {
 #define LVLIP_FLAT(UU, NTV, CG)                                                               \
     case UU * 4 + (NTV ? 2 : 0) + (CG ? 1 : 0):                                              \
-        hipLaunchKernelGGL((lvlip::k_flat2<UU, NTV, CG>), dim3(grid), dim3(lvlip::FT), 0, s,  \
-                           (const uint8_t*)base, descs, n, out);                             \
+        hipLaunchKernelGGL((lvlip::k_flat2<UU, NTV, CG, lvlip::DescSrc>), dim3(grid),         \
+                           dim3(lvlip::FT), 0, s, (const uint8_t*)base,                      \
+                           lvlip::DescSrc{descs, out}, n);                                  \
         break;
                 LVLIP_FLAT(2, true, true) LVLIP_FLAT(2, true, false)
                 LVLIP_FLAT(2, false, true) LVLIP_FLAT(2, false, false)
@@ -1850,3 +1855,42 @@ int lvlip_csum_batch_dev(const void* base, const lvlip_csum_desc* descs, uint32_
 }
 
 }  // extern "C"
+
+namespace {
+
+template <int MODE>
+int launch_frames(const void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* out8,
+                  hipStream_t s) {
+    using Src = lvlip::FrameSrc<MODE>;
+    // a dispatch holds at most 2^30 entries (kLaunchMax): whole frames per launch
+    const uint32_t per = kLaunchMax / Src::SLOTS;
+    for (uint32_t f0 = 0; f0 < n;) {
+        const uint32_t m = n - f0 < per ? n - f0 : per;
+        const uint32_t entries = m * Src::SLOTS;
+        const uint32_t grid = (uint32_t)(((uint64_t)entries + lvlip::FT - 1) / lvlip::FT);
+        Src src{(const uint8_t*)base, (uint8_t*)base, frames + f0, out8 ? out8 + f0 : nullptr};
+        hipLaunchKernelGGL((lvlip::k_flat2<4, true, true, Src>), dim3(grid), dim3(lvlip::FT), 0, s,
+                           (const uint8_t*)base, src, entries);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "k_flat2 (frames)");
+        f0 += m;
+    }
+    return LVLIP_OK;
+}
+
+}  // namespace
+
+// Shared with skb_dev.hip (hidden: -fvisibility=hidden keeps it internal): f1/f2
+// on device-resident frames as one fused flat-sweep launch (flat_src.h).
+// mode: 0 TX fill (out8 = status, may be null), 1 RX header verify, 2 RX with
+// L4 (out8 = verdict).
+int lvlip_internal_frames(int mode, const void* base, const lvlip_frame_desc* frames, uint32_t n,
+                          uint8_t* out8, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    switch (mode) {
+        case lvlip::FR_TX: return launch_frames<lvlip::FR_TX>(base, frames, n, out8, s);
+        case lvlip::FR_RX: return launch_frames<lvlip::FR_RX>(base, frames, n, out8, s);
+        case lvlip::FR_RX_L4: return launch_frames<lvlip::FR_RX_L4>(base, frames, n, out8, s);
+        default: return LVLIP_EINVAL;
+    }
+}

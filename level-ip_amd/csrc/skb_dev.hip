@@ -1,7 +1,10 @@
 // skb_dev.hip — f1/f2 of SURVEY.md §8f for frames already in HBM
 // (include/lvlip_skb.h, "device-resident frames").
 //
-// Same decisions as skb_batch.c (which cites the reference line of each), as
+// Default: one fused launch of the flat sweep whose phase 1 parses the frames
+// and whose phase 4 applies the results (FrameSrc, flat_src.h).  Kept as an A/B
+// path (LVLIP_FRAMES_3PASS=1) and as a cross-check in the tests: the same
+// decisions as skb_batch.c (which cites the reference line of each), as
 // three stream-ordered steps with no host round trip:
 //   plan   one thread per frame parses its Ethernet/IPv4 header bytes and
 //          writes its checksum descriptors at fixed slots (2i, 2i+1 when an L4
@@ -16,11 +19,15 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "lvlip_csum.h"
 #include "lvlip_skb.h"
 
 int lvlip_internal_hip_fail(hipError_t e, const char* what);  // csum_kernels.hip
+// the fused path (csum_kernels.hip, flat_src.h): mode 0 TX, 1 RX, 2 RX + L4
+int lvlip_internal_frames(int mode, const void* base, const lvlip_frame_desc* frames, uint32_t n,
+                          uint8_t* out8, void* stream);
 
 namespace {
 
@@ -193,6 +200,16 @@ Workspace carve(void* ws, uint32_t n) {
     return w;
 }
 
+// LVLIP_FRAMES_3PASS=1 (A/B, read once): the plan / batch / apply pipeline
+// below instead of the fused sweep (flat_src.h), which is the default.
+bool three_pass() {
+    static const bool v = [] {
+        const char* e = getenv("LVLIP_FRAMES_3PASS");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 int launched(const char* what) {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? LVLIP_OK : lvlip_internal_hip_fail(e, what);
@@ -214,6 +231,9 @@ int lvlip_rx_verify_dev(const void* base, const lvlip_frame_desc* frames, uint32
     if (!base || !frames || !verdict || !workspace || n > kMaxFrames ||
         ((uintptr_t)base & 15u) || ((uintptr_t)workspace & 15u))
         return LVLIP_EINVAL;
+    if (!three_pass())
+        return lvlip_internal_frames((flags & LVLIP_RX_VERIFY_L4) ? 2 : 1, base, frames, n, verdict,
+                                     stream);
     hipStream_t s = (hipStream_t)stream;
     const Workspace w = carve(workspace, n);
     const uint32_t grid = (uint32_t)(((uint64_t)n + 255u) / 256u);
@@ -235,6 +255,7 @@ int lvlip_tx_checksum_dev(void* base, const lvlip_frame_desc* frames, uint32_t n
     if (!base || !frames || !workspace || n > kMaxFrames || ((uintptr_t)base & 15u) ||
         ((uintptr_t)workspace & 15u))
         return LVLIP_EINVAL;
+    if (!three_pass()) return lvlip_internal_frames(0, base, frames, n, status, stream);
     hipStream_t s = (hipStream_t)stream;
     const Workspace w = carve(workspace, n);
     const uint32_t grid = (uint32_t)(((uint64_t)n + 255u) / 256u);
