@@ -1202,7 +1202,7 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
 
     // ---- phase 1: descriptors -> chunk counts, ranks, records, head bitmap
     uint32_t start_sum = 0, nch = 0, meta = 0, lo = 0, lastv = 16, ctx = 0;
-    uint64_t a0 = 0;
+    uint64_t a0 = 0;  // the entry's first byte is a0 + lo
     bool big = false;
     if (i_me < n) {
         const lvlip_csum_desc d = src.get(i_me, ctx);
@@ -1394,7 +1394,7 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
         }
         res = finish(start_sum, acc);
     }
-    src.put(i_me, res, ctx, i_me < n);
+    src.put(i_me, res, ctx, i_me < n, a0 + lo);
 }
 }  // namespace lvlip
 

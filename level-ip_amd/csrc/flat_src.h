@@ -3,8 +3,9 @@
 //
 //   get(i, ctx): entry i as {offset, len, start_sum}; ctx is a word the source
 //       wants back in put
-//   put(i, c, ctx, valid): called by every thread of the workgroup (valid =
-//       i < n), so a source may exchange results between neighbouring lanes
+//   put(i, c, ctx, valid, addr): called by every thread of the workgroup (valid =
+//       i < n), so a source may exchange results between neighbouring lanes;
+//       addr is the entry's first byte (when its len > 0)
 //
 // DescSrc is the plain batch of include/lvlip_csum.h: a descriptor array in, a
 // u16 array out.
@@ -25,7 +26,7 @@ struct DescSrc {
         ctx = 0;
         return descs[i];
     }
-    __device__ __forceinline__ void put(uint32_t i, uint16_t c, uint32_t, bool valid) const {
+    __device__ __forceinline__ void put(uint32_t i, uint16_t c, uint32_t, bool valid, uint64_t) const {
         if (valid) out[i] = c;
     }
 };
@@ -64,11 +65,74 @@ __device__ __forceinline__ lvlip_csum_desc fr_mk(uint64_t off, uint32_t len, uin
     return d;
 }
 
+// The header bytes a frame's decisions read, [12, 56) of the frame, from four
+// 16-B aligned loads issued together (instead of one dependent byte load per
+// field): A[j] = frame bytes 12+4j .. 15+4j, little-endian.  A chunk is read
+// only when it holds a byte of the frame, so it lies inside the frame buffer
+// (its length is rounded up to 16 B, include/lvlip_skb.h); bytes past the
+// frame's len read as whatever the chunk holds and are never used.
+struct FrWin {
+    uint32_t A[11];
+    // safe: a readable 16-B aligned address for a frame with no byte in the
+    // window (a chunk of the frame's own descriptor)
+    __device__ __forceinline__ void load(const uint8_t* h, uint32_t len, uint64_t safe) {
+        const uint64_t p = reinterpret_cast<uint64_t>(h) + 12u;
+        const uint64_t a = p & ~15ull, end = reinterpret_cast<uint64_t>(h) + len;
+        const uint64_t a0 = a < end ? a : len ? reinterpret_cast<uint64_t>(h) & ~15ull : safe;
+        // four loads back to back, no branch between them: a chunk past the
+        // frame reloads a valid one and is then zeroed
+        // (one asm statement, waited inside it: the compiler would otherwise
+        // sink each load into the branch that first reads it)
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        v4u c[4];
+        uint64_t ad[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ad[k] = a + 16u * k < end ? a + 16u * k : a0;
+        asm volatile(
+            "global_load_dwordx4 %0, %4, off\n\t"
+            "global_load_dwordx4 %1, %5, off\n\t"
+            "global_load_dwordx4 %2, %6, off\n\t"
+            "global_load_dwordx4 %3, %7, off\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3])
+            : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
+            : "memory");
+        uint32_t W[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t m = a + 16u * k < end ? 0xffffffffu : 0u;
+            W[4 * k] = c[k].x & m;
+            W[4 * k + 1] = c[k].y & m;
+            W[4 * k + 2] = c[k].z & m;
+            W[4 * k + 3] = c[k].w & m;
+        }
+        // L[j] = W[j + q] by bit selects (no divergent branch), then one
+        // alignbyte per output dword
+        const uint32_t q = (uint32_t)(p & 15u) >> 2, r = (uint32_t)p & 3u;
+        const uint32_t m1 = 0u - (q & 1u), m2 = 0u - (q >> 1);
+        uint32_t L[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const uint32_t t01 = (W[j] & ~m1) | (W[j + 1] & m1);
+            const uint32_t t23 = (W[j + 2] & ~m1) | (W[j + 3] & m1);
+            L[j] = (t01 & ~m2) | (t23 & m2);
+        }
+#pragma unroll
+        for (int j = 0; j < 11; ++j) A[j] = __builtin_amdgcn_alignbyte(L[j + 1], L[j], r);
+    }
+    // byte o of the frame, 12 <= o < 56 (o a constant)
+    __device__ __forceinline__ uint32_t b(uint32_t o) const { return (A[(o - 12u) >> 2] >> (8u * ((o - 12u) & 3u))) & 0xffu; }
+    __device__ __forceinline__ uint32_t be16(uint32_t o) const { return (b(o) << 8) | b(o + 1u); }
+    __device__ __forceinline__ uint32_t le16(uint32_t o) const { return b(o) | (b(o + 1u) << 8); }
+    __device__ __forceinline__ uint32_t le32(uint32_t o) const { return le16(o) | (le16(o + 2u) << 16); }
+};
+
 // The decisions are those of skb_batch.c (host), which cites the reference line
 // of each.  Entry slots: RX with L4 and TX use two per frame (lanes 2f, 2f+1 of
 // one wave, so the pair exchanges results by shuffle), RX header-only one.  An
-// entry the frame does not have is empty (len 0).  Frame bytes are read with
-// byte loads (any alignment), never past the frame's len.
+// entry the frame does not have is empty (len 0).  Header bytes come from the
+// FrWin window; a field outside it is read with byte loads, never past the
+// frame's len.
 template <int MODE>
 struct FrameSrc {
     const uint8_t* base;             // the frames' bytes
@@ -79,38 +143,37 @@ struct FrameSrc {
 
     // ip_rcv's decisions (src/ip_input.c:17-60) -> entries {header, L4} and the
     // plan word (verdict so far | flags)
-    __device__ __forceinline__ void parse_rx(const lvlip_frame_desc& fd, const uint8_t* h,
+    __device__ __forceinline__ void parse_rx(const lvlip_frame_desc& fd, const FrWin& x,
                                              lvlip_csum_desc& d0, lvlip_csum_desc& d1,
                                              uint32_t& w) const {
         uint32_t v = 0;
         if (fd.len < FR_ETH + 20u) {
             v = LVLIP_RX_SHORT;
-        } else if (fr_be16(h + 12) != 0x0800u) {  // netdev_receive, src/netdev.c:67-80
+        } else if (x.be16(12) != 0x0800u) {  // netdev_receive, src/netdev.c:67-80
             v = LVLIP_RX_NOT_IP;
         } else {
-            const uint32_t ver = h[14] >> 4, ihl = h[14] & 0x0fu;
+            const uint32_t ver = x.b(14) >> 4, ihl = x.b(14) & 0x0fu;
             if (ver != 4u) {  // src/ip_input.c:22
                 v = LVLIP_RX_BAD_VERSION;
             } else if (ihl < 5u) {  // src/ip_input.c:27
                 v = LVLIP_RX_BAD_IHL;
-            } else if (h[22] == 0u) {  // src/ip_input.c:32
+            } else if (x.b(22) == 0u) {  // src/ip_input.c:32
                 v = LVLIP_RX_TTL0;
             } else if (fd.len < FR_ETH + ihl * 4u) {
                 v = LVLIP_RX_SHORT;
             } else {
                 d0 = fr_mk(fd.offset + FR_ETH, ihl * 4u, 0);  // src/ip_input.c:38
                 w |= FR_HAS_HDR;
-                const uint32_t proto = h[23];
+                const uint32_t proto = x.b(23);
                 if (proto != 6u && proto != 1u) {  // src/ip_input.c:51-60
                     v = FR_PENDING | LVLIP_RX_UNKNOWN_PROTO;
                 } else if (MODE == FR_RX_L4) {
-                    const uint32_t iplen = fr_be16(h + 16);
+                    const uint32_t iplen = x.be16(16);
                     if (iplen < ihl * 4u || fd.len < FR_ETH + iplen) {
                         v = FR_PENDING | LVLIP_RX_SHORT;
                     } else {
                         const uint32_t l4len = iplen - ihl * 4u;
-                        const uint32_t seed =
-                            proto == 6u ? fr_pseudo_rfc(fr_le32(h + 26), fr_le32(h + 30), 6u, l4len) : 0u;
+                        const uint32_t seed = proto == 6u ? fr_pseudo_rfc(x.le32(26), x.le32(30), 6u, l4len) : 0u;
                         d1 = fr_mk(fd.offset + FR_ETH + ihl * 4u, l4len, seed);
                         w |= FR_HAS_L4;
                     }
@@ -120,38 +183,57 @@ struct FrameSrc {
         w |= v;
     }
 
-    // the TX decisions of lvlip_tx_plan -> entries {L4, header}; plan word =
-    // filled | L4 flag | the L4 checksum field's offset in the frame << 16
-    __device__ __forceinline__ void parse_tx(const lvlip_frame_desc& fd, const uint8_t* h,
+    // the TX decisions of lvlip_tx_plan -> entries {header, L4} (address order,
+    // as the sweep wants its entries); plan word =
+    // filled | L4 flag | the L4 checksum field's offset in the L4 entry << 16
+    __device__ __forceinline__ void parse_tx(const lvlip_frame_desc& fd, const uint8_t* h, const FrWin& x,
                                              lvlip_csum_desc& d0, lvlip_csum_desc& d1,
                                              uint32_t& w) const {
         if (fd.len < FR_ETH + 20u) return;
-        const uint32_t ihl = h[14] & 0x0fu, iplen = fr_be16(h + 16), proto = h[23];
-        if ((h[14] >> 4) != 4u || ihl < 5u || iplen < ihl * 4u || fd.len < FR_ETH + iplen) return;
+        const uint32_t ihl = x.b(14) & 0x0fu, iplen = x.be16(16), proto = x.b(23);
+        if ((x.b(14) >> 4) != 4u || ihl < 5u || iplen < ihl * 4u || fd.len < FR_ETH + iplen) return;
         const uint32_t l4 = FR_ETH + ihl * 4u, l4len = iplen - ihl * 4u;
         // each field's current u16 is taken out of the seed (skb_batch.c): the
-        // same sum as the reference's zero-then-checksum, mod 2^32
+        // same sum as the reference's zero-then-checksum, mod 2^32.  The L4
+        // field is in the window for ihl 5-6, else one more (dependent) read.
         if (proto == 6u && l4len >= 20u) {  // src/tcp_output.c:110,126
-            d0 = fr_mk(fd.offset + l4, l4len,
-                       fr_pseudo_lossy(fr_le32(h + 26), fr_le32(h + 30), 6u, l4len) - fr_le16(h + l4 + 16));
-            w = FR_HAS_L4 | ((l4 + 16u) << 16);
+            const uint32_t cur = ihl == 5u ? x.le16(50) : ihl == 6u ? x.le16(54) : fr_le16(h + l4 + 16);
+            d1 = fr_mk(fd.offset + l4, l4len, fr_pseudo_lossy(x.le32(26), x.le32(30), 6u, l4len) - cur);
+            w = FR_HAS_L4 | (16u << 16);
         } else if (proto == 1u && l4len >= 4u) {  // src/icmpv4.c:46-47
-            d0 = fr_mk(fd.offset + l4, l4len, 0u - fr_le16(h + l4 + 2));
-            w = FR_HAS_L4 | ((l4 + 2u) << 16);
+            const uint32_t cur = ihl == 5u ? x.le16(36) : ihl == 6u ? x.le16(40) : fr_le16(h + l4 + 2);
+            d1 = fr_mk(fd.offset + l4, l4len, 0u - cur);
+            w = FR_HAS_L4 | (2u << 16);
         }
-        d1 = fr_mk(fd.offset + FR_ETH, ihl * 4u, 0u - fr_le16(h + 24));  // src/ip_output.c:42,53
+        d0 = fr_mk(fd.offset + FR_ETH, ihl * 4u, 0u - x.le16(24));  // src/ip_output.c:42,53
         w |= 1u;
     }
 
     __device__ __forceinline__ lvlip_csum_desc get(uint32_t i, uint32_t& w) const {
-        const lvlip_frame_desc fd = frames[i / SLOTS];
+        // the descriptor's two words in flight together (the compiler would
+        // load len, branch on it, then load offset)
+        typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+        v2u fo, fl;
+        asm volatile(
+            "global_load_dwordx2 %0, %2, off\n\t"
+            "global_load_dwordx2 %1, %2, off offset:8\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(fo), "=&v"(fl)
+            : "v"(reinterpret_cast<uint64_t>(frames + i / SLOTS))
+            : "memory");
+        lvlip_frame_desc fd;
+        fd.offset = (uint64_t)fo.x | ((uint64_t)fo.y << 32);
+        fd.len = fl.x;
+        fd.reserved = 0;
         const uint8_t* h = base + fd.offset;
+        FrWin x;
+        x.load(h, fd.len, reinterpret_cast<uint64_t>(frames + i / SLOTS) & ~15ull);
         lvlip_csum_desc d0 = fr_mk(0, 0, 0), d1 = fr_mk(0, 0, 0);
         w = 0;
         if (MODE == FR_TX)
-            parse_tx(fd, h, d0, d1, w);
+            parse_tx(fd, h, x, d0, d1, w);
         else
-            parse_rx(fd, h, d0, d1, w);
+            parse_rx(fd, x, d0, d1, w);
         return (SLOTS == 2u && (i & 1u)) ? d1 : d0;
     }
 
@@ -159,22 +241,26 @@ struct FrameSrc {
     // neighbouring workgroup that reads those bytes as part of an edge chunk
     // adds and then subtracts the same value it read, so a concurrent write
     // cannot change its sums.
-    __device__ __forceinline__ void put(uint32_t i, uint16_t c, uint32_t w, bool valid) const {
+    // The field is addressed from the entry's own first byte (no second read of
+    // the frame descriptor): L4 field at entry + (w >> 16), IPv4 header
+    // checksum at entry + 10.
+    __device__ __forceinline__ void put(uint32_t i, uint16_t c, uint32_t w, bool valid,
+                                        uint64_t addr) const {
         const uint32_t f = i / SLOTS;
         if (MODE == FR_TX) {
             if (!valid) return;
             if ((i & 1u) == 0u && out8) out8[f] = (uint8_t)(w & 1u);
             if (!(w & 1u)) return;
-            uint8_t* h = wbase + frames[f].offset;
-            if ((i & 1u) == 0u) {
-                if (w & FR_HAS_L4) {  // raw store (no htons), byte by byte: any alignment
-                    const uint32_t fo = w >> 16;
-                    h[fo] = (uint8_t)c;
-                    h[fo + 1] = (uint8_t)(c >> 8);
-                }
+            const bool l4 = (i & 1u) != 0u;
+            if (l4 && !(w & FR_HAS_L4)) return;
+            // raw store (no htons) of the two bytes; one u16 store when aligned
+            const uint64_t fa = addr + (l4 ? (w >> 16) : 10u);
+            uint8_t* p = wbase + (fa - reinterpret_cast<uint64_t>(base));
+            if (fa & 1ull) {
+                p[0] = (uint8_t)c;
+                p[1] = (uint8_t)(c >> 8);
             } else {
-                h[24] = (uint8_t)c;
-                h[25] = (uint8_t)(c >> 8);
+                *reinterpret_cast<uint16_t*>(p) = c;
             }
             return;
         }
