@@ -1729,8 +1729,13 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         // stays within ~10 % elsewhere, so it is the choice when sizes are unknown.
         const int hint = cfg ? cfg->len_hint : 0;
         if (hint >= 512) {
+            // shapes from scripts/shape_sweep.py: MTU-sized
+            // packets run best at 8 waves/CU with 3 in flight per wave
+            // (~36 KiB per CU), jumbo at 8 waves with 2 pieces, the rest at 16
             kernel = LVLIP_KERNEL_WAVE;
-            if (wpc <= 0) wpc = hint >= 4096 ? 8 : 16;
+            const bool mtu = hint >= 1280 && hint < 2048;
+            if (wpc <= 0) wpc = (hint >= 4096 || mtu) ? 8 : 16;
+            if (unroll <= 0 && mtu) unroll = 3;
         } else {
             kernel = LVLIP_KERNEL_FLAT;
         }
