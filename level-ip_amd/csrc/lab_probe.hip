@@ -53,6 +53,28 @@ __global__ __launch_bounds__(256) void k_probe(const uint4* __restrict__ src, ui
             for (int u = 0; u < U; ++u) acc += words(v[u]);
         }
         for (; i < n16; i += stride) acc += words(ld<NT>(src + i));
+    } else if (MODE == 4) {
+        // packetized like k_stream on tcp1500: 1504-B slots, each read as one full
+        // 1 KiB wave-load plus one with lanes 0..29 (the 476-B rest); U packets in
+        // flight per wave, wave-contiguous packet ranges
+        const uint64_t pk = n16 / 94;
+        const uint64_t nw = (uint64_t)gridDim.x * wpb;
+        const uint64_t per = (pk + nw - 1) / nw;
+        const uint64_t lo = ((uint64_t)blockIdx.x * wpb + wid) * per;
+        const uint64_t hi = lo + per < pk ? lo + per : pk;
+        const bool part = lane < 30u;
+        uint64_t p = lo;
+        for (; p + U <= hi; p += U) {
+            uint4 v[2 * U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                v[2 * u] = ld<NT>(src + (p + u) * 94 + lane);
+                v[2 * u + 1] = ld<NT>(src + (p + u) * 94 + 64 + (part ? lane : 29u));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += words(v[2 * u]) + (part ? words(v[2 * u + 1]) : 0u);
+        }
+        for (; p < hi; ++p) acc += words(ld<NT>(src + p * 94 + lane));
     } else {
         const uint64_t pieces = n16 / 64;  // 1 KiB pieces
         uint64_t lo, hi, step, first;
@@ -212,6 +234,7 @@ extern "C" int lvlip_lab_probe(const void* src, uint64_t bytes, uint32_t* sink, 
     CASES(0, 1) CASES(0, 2) CASES(0, 4) CASES(0, 8)
     CASES(1, 1) CASES(1, 2) CASES(1, 4) CASES(1, 8)
     CASES(2, 1) CASES(2, 2) CASES(2, 4) CASES(2, 8)
+    CASES(4, 1) CASES(4, 2) CASES(4, 3) CASES(4, 4)
 #undef CASES
 #undef CASE
     if (mode == 3) {
