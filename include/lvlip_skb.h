@@ -117,11 +117,11 @@ uint32_t lvlip_icmp_echo_reply_fill(lvlip_frame *frames, uint32_t n);
 
 /* Frames already in HBM (a receive ring filled by a GPU-direct NIC, or frames
  * built on the GPU): one frame = `len` bytes at base + offset, Ethernet header
- * first.  All three steps (plan, checksum batch, apply) run as kernels on the
- * caller's stream; nothing returns to the host.  Pointers are device
- * pointers; `base` is 16-B aligned and readable up to the last frame's end
- * rounded up to 16 B.  `workspace` holds lvlip_frames_workspace_bytes(n)
- * bytes of device memory, 16-B aligned. */
+ * first.  Parse, checksum and apply run as one kernel on the caller's stream;
+ * nothing returns to the host.  Pointers are device pointers; `base` is 16-B
+ * aligned and readable up to the last frame's end rounded up to 16 B.
+ * `workspace` is reserved and may be NULL: lvlip_frames_workspace_bytes()
+ * returns 0 (ABI 1 kept the argument from the earlier three-kernel form). */
 typedef struct lvlip_frame_desc {
     uint64_t offset;
     uint32_t len;

@@ -360,8 +360,7 @@ def _frames_dev(base, fdescs):
     if not hasattr(fdescs, "numel"):
         fdescs = torch.from_numpy(np.ascontiguousarray(fdescs, dtype=FRAME_DESC_DTYPE)
                                   .view(np.uint8).copy()).to(base.device)
-    ws = torch.empty(int(_lib.lvlip_frames_workspace_bytes(n)), dtype=torch.uint8, device=base.device)
-    return n, fdescs, ws
+    return n, fdescs
 
 
 def rx_verify_dev(base, fdescs, flags: int = 0, stream=None):
@@ -369,11 +368,11 @@ def rx_verify_dev(base, fdescs, flags: int = 0, stream=None):
     (uint8 CUDA tensor), asynchronously on `stream` (default: current)."""
     import torch
 
-    n, fd, ws = _frames_dev(base, fdescs)
+    n, fd = _frames_dev(base, fdescs)
     verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=base.device)
     s = stream or torch.cuda.current_stream(base.device)
     _check(_lib.lvlip_rx_verify_dev(base.data_ptr(), fd.data_ptr(), n, flags, verdict.data_ptr(),
-                                    ws.data_ptr(), s.cuda_stream), "lvlip_rx_verify_dev")
+                                    None, s.cuda_stream), "lvlip_rx_verify_dev")
     return verdict[:n]
 
 
@@ -382,11 +381,11 @@ def tx_checksum_dev(base, fdescs, stream=None):
     the per-frame status (1 filled, 0 malformed and untouched)."""
     import torch
 
-    n, fd, ws = _frames_dev(base, fdescs)
+    n, fd = _frames_dev(base, fdescs)
     status = torch.empty(max(n, 1), dtype=torch.uint8, device=base.device)
     s = stream or torch.cuda.current_stream(base.device)
     _check(_lib.lvlip_tx_checksum_dev(base.data_ptr(), fd.data_ptr(), n, status.data_ptr(),
-                                      ws.data_ptr(), s.cuda_stream), "lvlip_tx_checksum_dev")
+                                      None, s.cuda_stream), "lvlip_tx_checksum_dev")
     return status[:n]
 
 
