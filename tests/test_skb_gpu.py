@@ -160,3 +160,27 @@ def test_tx_dev_then_rx_dev_roundtrip_large():
     with lvlip.Context(0) as ctx:
         assert np.array_equal(ctx.rx_verify(filled, lvlip.RX_VERIFY_L4), v)
     assert (v == lvlip.RX_OK).mean() > 0.4 and set(np.unique(v)) <= {lvlip.RX_OK, lvlip.RX_BAD_L4}
+
+
+def test_dev_frames_arguments():
+    """Argument errors return LVLIP_EINVAL before any launch; n = 0 is a no-op;
+    the reserved workspace may be NULL (its size is 0)."""
+    lib = lvlip.lib()
+    assert lib.lvlip_frames_workspace_bytes(1000) == 0
+    fr = workloads.frames(8, seed=57)
+    buf, fd = lvlip.pack_frames(fr, align_mod=1)
+    base = _dev(np.concatenate([buf, np.zeros(32, np.uint8)]))
+    fdt = torch.from_numpy(fd.view(np.uint8).copy()).cuda()
+    out = torch.zeros(8, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    p, f, o = base.data_ptr(), fdt.data_ptr(), out.data_ptr()
+    assert lib.lvlip_rx_verify_dev(p + 1, f, 8, 0, o, None, s) == lvlip.EINVAL  # base not 16-B aligned
+    assert lib.lvlip_rx_verify_dev(p, None, 8, 0, o, None, s) == lvlip.EINVAL
+    assert lib.lvlip_rx_verify_dev(p, f, 8, 0, None, None, s) == lvlip.EINVAL  # verdict required
+    assert lib.lvlip_tx_checksum_dev(None, f, 8, o, None, s) == lvlip.EINVAL
+    assert lib.lvlip_rx_verify_dev(p, f, 0, 0, None, None, s) == lvlip.OK      # n = 0
+    assert lib.lvlip_tx_checksum_dev(p, f, 8, None, None, s) == lvlip.OK       # status optional
+    torch.cuda.synchronize()
+    assert lib.lvlip_rx_verify_dev(p, f, 8, 0, o, None, s) == lvlip.OK  # headers filled above
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tolist() == [lvlip.RX_OK] * 8
