@@ -398,6 +398,33 @@ def frames_dev(lvlip, torch, dev):
     v = lvlip.rx_verify_dev(base, fdt, 0, stream=stream)
     torch.cuda.synchronize(dev)
     res["rx_header_all_ok"] = bool((v == lvlip.RX_OK).all())
+    # the same frames from host memory through the host API (PCIe-inclusive:
+    # plan on the CPU, gather, H2D, kernel, D2H, apply), on a 512K-frame prefix
+    import ctypes
+
+    nh = min(n, 1 << 19)
+    end = int(fd["offset"][nh - 1]) + int(fd["len"][nh - 1])
+    host = base[: (end + 15) // 16 * 16].cpu().numpy().copy()
+    fr = np.zeros(nh, dtype=[("head", "<u8"), ("len", "<u4"), ("pad", "<u4")])
+    assert fr.dtype.itemsize == ctypes.sizeof(lvlip.Frame)
+    fr["head"] = host.ctypes.data + fd["offset"][:nh]
+    fr["len"] = fd["len"][:nh]
+    arr = ctypes.cast(fr.ctypes.data, ctypes.POINTER(lvlip.Frame))
+    verdict = np.zeros(nh, np.uint8)
+    hl4 = int(pay["len"][:nh].sum())
+    lib = lvlip.lib()
+    with lvlip.Context(dev.index or 0) as ctx:
+        for name, call, nbytes in (
+                ("host_tx_fill", lambda: lib.lvlip_tx_checksum(ctx._h, arr, nh), 20 * nh + hl4),
+                ("host_rx_header_l4", lambda: lib.lvlip_rx_verify(ctx._h, arr, nh, lvlip.RX_VERIFY_L4,
+                                                                 verdict.ctypes.data), 20 * nh + hl4)):
+            assert call() == 0, name
+            t0 = time.perf_counter()
+            for _ in range(3):
+                assert call() == 0, name
+            ms = (time.perf_counter() - t0) / 3 * 1e3
+            res[name] = {"frames": nh, "ms": round(ms, 3), "Mframes_per_s": round(nh / ms / 1e3, 2),
+                         "GBps": round(nbytes / ms / 1e6, 2)}
     log("device-resident frames", res)
     return res
 

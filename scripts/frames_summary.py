@@ -42,7 +42,9 @@ def main():
     n = b.descs.size // 2
     l4 = int(b.descs[1::2]["len"].sum())
     algo = {"tx_fill": 20 * n + l4 + 5 * n, "rx_header": 20 * n + n, "rx_header_l4": 20 * n + l4 + n}
-    trace = dispatches(os.path.join(prof, "trace", "trace_kernel_trace.csv"))
+    # the device calls come first; later k_flat2 launches (the host-API timings
+    # of bench.py --frames) are not part of this summary
+    trace = dispatches(os.path.join(prof, "trace", "trace_kernel_trace.csv"))[: len(MODES)]
     assert len(trace) == len(MODES), (len(trace), len(MODES))
     per = {m: {"dur_ns": [], "grid": set()} for m in algo}
     for r, m in zip(trace, MODES):
@@ -50,7 +52,7 @@ def main():
         per[m]["grid"].add(int(r["Grid_Size_X"]))
     assert per["rx_header"]["grid"] == {256 * ((n + 255) // 256)}, per["rx_header"]["grid"]
     for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
-        rows = dispatches(os.path.join(prof, sub, f"{sub}_counter_collection.csv"))
+        rows = dispatches(os.path.join(prof, sub, f"{sub}_counter_collection.csv"))[: len(MODES)]
         assert len(rows) == len(MODES), (sub, len(rows))
         for r, m in zip(rows, MODES):
             per[m].setdefault(counter, []).append(float(r["Counter_Value"]))
