@@ -228,11 +228,13 @@ def _ip_hdr(src, dst, proto, payload_len, ident):
     return bytes(h)
 
 
-def echo_child(out_path: str):
+def echo_child(out_path: str, so_path: str = pyoracle.REF_SO):
     """Runs in a subprocess: fd 0 becomes one end of a socketpair (the stack's
     tun fd is a zero-initialised static, src/tuntap_if.c:5, so tun_write writes
-    to fd 0, src/tuntap_if.c:68-71)."""
-    lib = ctypes.CDLL(pyoracle.REF_SO)
+    to fd 0, src/tuntap_if.c:68-71).  `so_path` is the reference stack to drive:
+    libref.so for the fixtures, libref_dropin.so (the same objects on the
+    product library's checksum) for tests/test_ref_stack_dropin.py."""
+    lib = ctypes.CDLL(so_path)
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
     os.dup2(a.fileno(), 0)
     lib.netdev_init()           # 10.0.0.4 / 00:0c:29:6d:50:25 (src/netdev.c:34-38)
@@ -279,7 +281,7 @@ def main():
 
 
 if __name__ == "__main__":
-    if len(sys.argv) == 3 and sys.argv[1] == "--echo-child":
-        echo_child(sys.argv[2])
+    if len(sys.argv) in (3, 4) and sys.argv[1] == "--echo-child":
+        echo_child(*sys.argv[2:])
     else:
         main()
