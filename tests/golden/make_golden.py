@@ -10,10 +10,13 @@ the oracle and the GPU path against these files with no reference present.
   vectors.npz  seeded random + adversarial checksum() cases (any offset/len/seed)
   tcp.npz      tcp_udp_checksum() cases (src/tcp.c:87-98), incl. the lost carry
   iphdr.npz    ip_send_check() cases (src/ip_output.c:8-12), ihl 5..15
-  echo.npz     config #1: ICMPv4 echo request -> reply frames produced by the
+  echo.json    config #1: ICMPv4 echo request -> reply frames produced by the
                reference stack (ip_rcv -> icmpv4_reply -> ip_output ->
                netdev_transmit -> tun_write) through an in-memory fake TAP
                (a socketpair dup'ed onto the stack's tun fd)
+  tcp_frames.json  TCP frames the reference stack transmits (SYN with options,
+               retransmit, 536/536/536/393-B data segments, ACK, RST) through
+               the same fake TAP (tests/ref_stack_child.py on libref.so)
 
 usage: python tests/golden/make_golden.py   (from the repo root)
 """
@@ -275,6 +278,9 @@ def main():
     np.savez_compressed(os.path.join(OUT, "tcp.npz"), **make_tcp(lib, rng))
     np.savez_compressed(os.path.join(OUT, "iphdr.npz"), **make_iphdr(lib, rng))
     subprocess.run([sys.executable, __file__, "--echo-child", os.path.join(OUT, "echo.json")],
+                   check=True, stdin=subprocess.DEVNULL)
+    subprocess.run([sys.executable, os.path.join(os.path.dirname(OUT), "ref_stack_child.py"),
+                    os.path.join(OUT, "tcp_frames.json"), pyoracle.REF_SO],
                    check=True, stdin=subprocess.DEVNULL)
     for fn in sorted(os.listdir(OUT)):
         print(fn, os.path.getsize(os.path.join(OUT, fn)))

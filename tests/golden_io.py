@@ -44,3 +44,10 @@ def iphdr():
 def echo():
     with open(os.path.join(GOLDEN, "echo.json")) as f:
         return json.load(f)
+
+
+def tcp_frames():
+    """TCP frames the reference stack transmitted (tests/ref_stack_child.py)."""
+    with open(os.path.join(GOLDEN, "tcp_frames.json")) as f:
+        d = json.load(f)
+    return [bytes.fromhex(h) for h in d["frames"]]

@@ -97,6 +97,29 @@ def test_tx_echo_reply_golden():
         assert bytes(f) == bytes.fromhex(case["reply_hex"])
 
 
+def _scrambled_tcp_frames():
+    want = golden_io.tcp_frames()
+    fr = []
+    for k, w in enumerate(want):
+        f = bytearray(w)
+        f[24:26] = (b"\0\0", b"\xff\xff", b"\xde\xad")[k % 3]
+        f[34 + 16:34 + 18] = (b"\xff\xff", b"\0\0", b"\xbe\xef")[k % 3]
+        fr.append(f)
+    return fr, want
+
+
+def test_tx_tcp_stack_frames_golden():
+    """f2 on the frames level-ip's own TCP transmit path wrote
+    (tests/golden/tcp_frames.json: SYN with MSS/SACK/WS options, data segments
+    of 536/536/536/393 B, ACK, RST): fields scrambled, refilled by plan/apply ==
+    the reference's bytes; and RX verify (header + L4) accepts them."""
+    fr, want = _scrambled_tcp_frames()
+    tx_via_plan(fr)
+    assert [bytes(f) for f in fr] == want
+    for flags in (0, lvlip.RX_VERIFY_L4):
+        assert rx_via_plan(fr, flags).tolist() == [lvlip.RX_OK] * len(fr)
+
+
 def test_tx_tcp_golden_segments():
     """TCP TX over the segments of tests/golden/tcp.npz (reference
     tcp_udp_checksum outputs): with the field restored to the value the golden

@@ -9,7 +9,7 @@ import golden_io
 import lvlip
 import skb_oracle
 import workloads
-from test_skb_cpu import _rx_cases
+from test_skb_cpu import _rx_cases, _scrambled_tcp_frames
 
 pytestmark = pytest.mark.gpu
 
@@ -57,6 +57,25 @@ def test_tx_echo_reply_golden(ctx):
         fr.append(rep)
     ctx.tx_checksum(fr)
     assert [bytes(f) for f in fr] == [bytes.fromhex(c["reply_hex"]) for c in e]
+
+
+def test_tx_tcp_stack_frames_golden(ctx):
+    """The reference TCP transmit path's frames (tests/golden/tcp_frames.json),
+    fields scrambled, refilled by the GPU batch == the reference's bytes, on the
+    host-resident path and on the device-resident one; RX verify accepts them."""
+    fr, want = _scrambled_tcp_frames()
+    ctx.tx_checksum(fr)
+    assert [bytes(f) for f in fr] == want
+    assert ctx.rx_verify(fr, lvlip.RX_VERIFY_L4).tolist() == [lvlip.RX_OK] * len(fr)
+    fr, _ = _scrambled_tcp_frames()
+    buf, fd = lvlip.pack_frames(fr, align_mod=16, seed=3)
+    base = _dev(buf)
+    assert lvlip.tx_checksum_dev(base, fd).cpu().numpy().tolist() == [1] * len(fr)
+    out = base.cpu().numpy()
+    got = [out[int(d["offset"]):int(d["offset"]) + int(d["len"])].tobytes() for d in fd]
+    assert got == want
+    v = lvlip.rx_verify_dev(base, fd, lvlip.RX_VERIFY_L4).cpu().numpy()
+    assert v.tolist() == [lvlip.RX_OK] * len(fr)
 
 
 def test_tx_malformed_untouched(ctx):
