@@ -1,0 +1,65 @@
+"""The library's host C code under ASan + UBSan and under TSan (SURVEY.md §5:
+level-ip's `make debug` is a -fsanitize=thread build, Makefile:17-18, and its
+runner greps ThreadSanitizer reports, tests/test-run-all:41).
+
+tests/sanitize/host_san.c drives level-ip_amd/csrc/csum_cpu.c (the per-call
+drop-in, AVX2 and portable paths) and level-ip_amd/csrc/skb_batch.c (the frame
+calls' multi-threaded host steps) against the oracle; see its header.  Host
+code only: GPU sanitizers are not available on the MI355X pool."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRCS = [os.path.join(ROOT, p) for p in (
+    "level-ip_amd/csrc/csum_cpu.c", "level-ip_amd/csrc/skb_batch.c",
+    "oracle/csum_oracle.c", "tests/sanitize/host_san.c")]
+FLAGS = {
+    "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"],
+    "tsan": ["-fsanitize=thread"],
+}
+REPORTS = ("ERROR: AddressSanitizer", "runtime error:", "WARNING: ThreadSanitizer",
+           "ERROR: LeakSanitizer")
+
+
+def _build(kind, tmp_path):
+    cc = shutil.which("gcc")
+    if cc is None:
+        pytest.skip("gcc not available")
+    exe = str(tmp_path / f"host_{kind}")
+    r = subprocess.run([cc, "-O1", "-g", "-pthread", "-I", os.path.join(ROOT, "include"),
+                        *FLAGS[kind], *SRCS, "-o", exe], capture_output=True, text=True)
+    if r.returncode != 0 and "cannot find" in r.stderr:
+        pytest.skip(f"{kind} runtime not installed: {r.stderr.strip()[:200]}")
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def _check(r):
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert not [k for k in REPORTS if k in out], out[-4000:]
+    assert "all checks passed" in r.stdout
+
+
+@pytest.mark.parametrize("scalar", ["0", "1"])
+def test_host_code_asan_ubsan(tmp_path, scalar):
+    exe = _build("asan", tmp_path)
+    env = dict(os.environ, LVLIP_CPU_SCALAR=scalar)
+    _check(subprocess.run([exe], capture_output=True, text=True, env=env, timeout=600))
+
+
+def test_host_code_tsan(tmp_path):
+    exe = _build("tsan", tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    if r.returncode != 0 and "unexpected memory mapping" in r.stderr:
+        # gcc 11's TSan cannot place its shadow under some kernels' ASLR layout;
+        # its documented remedy is to run with address randomisation off
+        setarch = shutil.which("setarch")
+        if setarch is None:
+            pytest.skip("TSan needs ASLR off and setarch is absent")
+        r = subprocess.run([setarch, os.uname().machine, "-R", exe],
+                           capture_output=True, text=True, timeout=600)
+    _check(r)
