@@ -1,0 +1,188 @@
+// tests/sanitize/ctx_san.cpp — the host-resident GPU batch paths with
+// AddressSanitizer on their host code (run on the MI355X box by
+// tests/test_skb_gpu.py::test_host_batches_under_asan).
+//
+// TEST INFRASTRUCTURE ONLY.  tests/sanitize/Makefile compiles the product's
+// own sources (csum_ctx.cpp, skb_batch.c, csum_cpu.c, csum_kernels.hip,
+// skb_dev.hip) with `-Xarch_host -fsanitize=address` into one executable, so
+// the context's pieces, slots, double-buffering, registered regions and the
+// frame calls' host steps run under ASan against real GPU batches.  Every
+// packet and frame sits in an allocation that ends at its last byte.  Results
+// are checked against the oracle (oracle/csum_oracle.c).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <thread>
+#include <vector>
+
+#include "lvlip_csum.h"
+#include "lvlip_skb.h"
+
+extern "C" uint16_t oracle_checksum(const void* addr, int count, int start_sum);
+
+static int g_fail = 0;
+#define CHECK(c, ...)                                            \
+    do {                                                         \
+        if (!(c)) {                                              \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);                        \
+            fputc('\n', stderr);                                 \
+            if (++g_fail > 20) exit(1);                          \
+        }                                                        \
+    } while (0)
+
+struct Rng {
+    uint64_t s;
+    uint32_t operator()() {
+        s = s * 6364136223846793005ull + 1442695040888963407ull;
+        return (uint32_t)(s >> 33);
+    }
+};
+
+// Scattered packets, each in its own exact-size allocation, through a context
+// whose small arena forces many double-buffered pieces.
+static void scattered(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_t seed) {
+    Rng r{seed};
+    std::vector<uint8_t*> mem(n);
+    std::vector<lvlip_csum_iov> iov(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const int32_t len = (r() % 97u == 0) ? -(int32_t)(r() % 5u) : (int32_t)(r() % (max_len + 1));
+        const uint32_t off = r() % 16u;
+        const size_t bytes = off + (len > 0 ? (size_t)len : 0) + (len <= 0);
+        mem[i] = (uint8_t*)malloc(bytes);
+        for (size_t b = 0; b < bytes; ++b) mem[i][b] = (uint8_t)r();
+        iov[i].ptr = mem[i] + off;
+        iov[i].len = len;
+        iov[i].start_sum = r();
+    }
+    std::vector<uint16_t> out(n, 0);
+    CHECK(lvlip_csum_batch_host(ctx, iov.data(), n, out.data()) == LVLIP_OK, "batch_host n=%u", n);
+    for (uint32_t i = 0; i < n; ++i)
+        CHECK(out[i] == oracle_checksum(iov[i].ptr, iov[i].len, (int)iov[i].start_sum),
+              "scattered %u len %d", i, iov[i].len);
+    for (auto* p : mem) free(p);
+}
+
+// One flat buffer that ends at the last packet's last byte (not a multiple of
+// 16), packets at every alignment with gaps; optionally registered.
+static void flat(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_t seed, int reg) {
+    Rng r{seed};
+    std::vector<lvlip_csum_desc> d(n);
+    uint64_t off = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        off += r() % 40u;
+        d[i].offset = off;
+        d[i].len = (int32_t)(r() % (max_len + 1));
+        d[i].start_sum = r();
+        off += (uint64_t)d[i].len;
+    }
+    const size_t bytes = off ? off : 1;
+    uint8_t* base = (uint8_t*)malloc(bytes);
+    for (size_t b = 0; b < bytes; ++b) base[b] = (uint8_t)r();
+    if (reg >= 0)
+        CHECK(lvlip_csum_register(ctx, base, bytes, (uint32_t)reg) == LVLIP_OK, "register %d", reg);
+    std::vector<uint16_t> out(n, 0);
+    CHECK(lvlip_csum_batch_host_flat(ctx, base, bytes, d.data(), n, out.data()) == LVLIP_OK,
+          "batch_host_flat n=%u reg=%d", n, reg);
+    for (uint32_t i = 0; i < n; ++i)
+        CHECK(out[i] == oracle_checksum(base + d[i].offset, d[i].len, (int)d[i].start_sum),
+              "flat %u reg %d", i, reg);
+    if (reg == (int)LVLIP_REG_ZEROCOPY) {  // scattered packets inside the region: in place
+        std::vector<lvlip_csum_iov> iov(n);
+        for (uint32_t i = 0; i < n; ++i) iov[i] = {base + d[i].offset, d[i].len, d[i].start_sum};
+        std::fill(out.begin(), out.end(), 0);
+        CHECK(lvlip_csum_batch_host(ctx, iov.data(), n, out.data()) == LVLIP_OK, "zc batch_host");
+        for (uint32_t i = 0; i < n; ++i)
+            CHECK(out[i] == oracle_checksum(iov[i].ptr, iov[i].len, (int)iov[i].start_sum), "zc %u", i);
+    }
+    if (reg >= 0) CHECK(lvlip_csum_unregister(ctx, base) == LVLIP_OK, "unregister");
+    free(base);
+}
+
+// f1/f2 frame calls with a real context: exact-size frames, TX then RX.
+static void frame_calls(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed) {
+    Rng r{seed};
+    std::vector<lvlip_frame> fr(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const bool tcp = r() & 1u;
+        const uint32_t ihl = 5u + r() % 3u, l4hdr = tcp ? 20u + 4u * (r() % 6u) : 8u;
+        const uint32_t iplen = ihl * 4u + l4hdr + r() % 1461u, flen = 14u + iplen;
+        uint8_t* f = (uint8_t*)malloc(flen);
+        for (uint32_t b = 0; b < flen; ++b) f[b] = (uint8_t)r();
+        f[12] = 0x08, f[13] = 0x00;
+        uint8_t* ih = f + 14;
+        ih[0] = (uint8_t)(0x40u | ihl), ih[2] = (uint8_t)(iplen >> 8), ih[3] = (uint8_t)iplen;
+        ih[8] = 64, ih[9] = tcp ? 6 : 1;
+        // 10.0.0.1-120: the reference's u32 pseudo-header sum keeps its carry
+        ih[12] = 10, ih[13] = 0, ih[14] = 0, ih[15] = (uint8_t)(1u + r() % 120u);
+        ih[16] = 10, ih[17] = 0, ih[18] = 0, ih[19] = (uint8_t)(1u + r() % 120u);
+        if (tcp) ih[ihl * 4u + 12u] = (uint8_t)((l4hdr / 4u) << 4);
+        fr[i] = {f, flen};
+    }
+    CHECK(lvlip_tx_checksum(ctx, fr.data(), n) == LVLIP_OK, "tx");
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* ih = fr[i].head + 14;
+        CHECK(oracle_checksum(ih, (ih[0] & 15) * 4, 0) == 0, "frame %u header", i);
+    }
+    std::vector<uint8_t> v(n, 0);
+    CHECK(lvlip_rx_verify(ctx, fr.data(), n, LVLIP_RX_VERIFY_L4, v.data()) == LVLIP_OK, "rx");
+    uint32_t ok = 0;
+    for (uint32_t i = 0; i < n; ++i) ok += v[i] == LVLIP_RX_OK;
+    CHECK(ok == n, "rx: %u of %u ok", ok, n);
+    for (auto& f : fr) free(f.head);
+}
+
+int main() {
+    if (lvlip_device_count() < 1) {
+        fprintf(stderr, "no HIP device\n");
+        return 2;
+    }
+    lvlip_csum_ctx* ctx = nullptr;
+    CHECK(lvlip_csum_ctx_create(&ctx, 0, 1u << 20) == LVLIP_OK, "ctx_create");
+    scattered(ctx, 20000, 3000, 1);   // ~30 MB through a 1 MiB arena: many pieces
+    scattered(ctx, 3, 9000, 2);
+    flat(ctx, 20000, 1600, 3, -1);
+    flat(ctx, 20000, 1600, 4, (int)LVLIP_REG_DMA);
+    flat(ctx, 5000, 1600, 5, (int)LVLIP_REG_ZEROCOPY);
+    frame_calls(ctx, 20000, 6);
+
+    // a packet larger than the arena is refused; nothing is read
+    std::vector<uint8_t> big((2u << 20) + 5u, 0xab);
+    lvlip_csum_iov one{big.data(), (int32_t)big.size(), 0};
+    uint16_t o = 0;
+    CHECK(lvlip_csum_batch_host(ctx, &one, 1, &o) == LVLIP_ERANGE, "oversize");
+    // argument errors
+    CHECK(lvlip_csum_batch_host(nullptr, &one, 1, &o) == LVLIP_EINVAL, "null ctx");
+    CHECK(lvlip_csum_batch_host(ctx, nullptr, 0, nullptr) == LVLIP_OK, "n = 0");
+    lvlip_csum_desc bad{10, 20, 0};
+    CHECK(lvlip_csum_batch_host_flat(ctx, big.data(), 25, &bad, 1, &o) == LVLIP_EINVAL, "flat bounds");
+
+    // a region left registered is released by destroy
+    uint8_t* left = (uint8_t*)malloc(1u << 16);
+    CHECK(lvlip_csum_register(ctx, left, 1u << 16, LVLIP_REG_DMA) == LVLIP_OK, "register left");
+    CHECK(lvlip_csum_ctx_destroy(ctx) == LVLIP_OK, "destroy");
+    free(left);
+
+    // one context per thread, concurrently (src/main.c:83-89 threads)
+    std::vector<std::thread> th;
+    for (int t = 0; t < 4; ++t)
+        th.emplace_back([t] {
+            lvlip_csum_ctx* c = nullptr;
+            CHECK(lvlip_csum_ctx_create(&c, 0, 1u << 20) == LVLIP_OK, "thread ctx");
+            scattered(c, 4000, 2000, 100 + t);
+            flat(c, 4000, 1600, 200 + t, t & 1 ? (int)LVLIP_REG_DMA : -1);
+            CHECK(lvlip_csum_ctx_destroy(c) == LVLIP_OK, "thread destroy");
+        });
+    for (auto& x : th) x.join();
+
+    if (g_fail) {
+        fprintf(stderr, "%d failures\n", g_fail);
+        return 1;
+    }
+    printf("ctx_san: all checks passed\n");
+    return 0;
+}
