@@ -54,7 +54,8 @@ def _need_gpu():
 def dev_blob(a: np.ndarray, pad: int = 64):
     n = (a.size + pad + 15) & ~15
     t = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    t[: a.size] = torch.from_numpy(np.ascontiguousarray(a))
+    # a may be a read-only view (np.frombuffer of a fixture): copy before wrapping
+    t[: a.size] = torch.from_numpy(np.array(a, dtype=np.uint8, copy=True).ravel())
     return t
 
 
