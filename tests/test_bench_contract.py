@@ -1,0 +1,88 @@
+"""The bench line's contract, checked two ways.
+
+* CPU: the committed evidence (`profiles/r01_bench_tcp1500.json` and the rocprof
+  summary of the same command) is self-consistent -- the fields the driver and
+  the judge read are present, `value`/`roofline` follow from the byte count and
+  the timings, and the trace's average k_stream duration agrees with the line's
+  `roofline.kernel_ms`.
+* GPU: a short `bench.py` run prints one line of the same shape.
+"""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(ROOT, "profiles")
+METRIC = "device-resident checksum GB/s over packet batch; % of HBM-read roofline"
+TCP1500_BYTES = 1_048_576 * 1500
+
+
+def check_line(line: dict, steps: int, warmup: int):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline"):
+        assert k in line, k
+    assert line["metric"] == METRIC
+    assert line["unit"] == "GB/s" and line["higher_is_better"] is True
+    assert line["steps"] == steps and line["warmup"] == warmup
+    assert line["scaling"] == "weak" and line["vs_baseline"] is None
+    assert line["dtype"] == "u16"
+    assert "workload" in line["config"] and "model" not in line["config"]
+    assert line["verified_bit_exact"] is True
+    r = line["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=2e-3)
+    # achieved = algorithmic bytes per launch / the kernel's average launch time
+    assert r["achieved"] == pytest.approx(
+        r["algo_bytes_per_launch"] / (r["kernel_ms"] * 1e-3) / 1e9, rel=2e-3)
+    # value = whole-job bytes / wall time per step (HIP event timing sits inside it)
+    total = line["config"]["bytes_per_gpu"] * line["n_gpus"]
+    assert line["value"] == pytest.approx(total / (line["ms_per_step"] * 1e-3) / 1e9,
+                                          rel=5e-3)
+    assert line["value"] <= r["achieved"] * 1.01
+
+
+def test_committed_bench_line_consistent():
+    with open(os.path.join(PROF, "r01_bench_tcp1500.json")) as f:
+        line = json.loads(f.read().strip().splitlines()[-1])
+    check_line(line, steps=200, warmup=50)
+    assert line["n_gpus"] == 1
+    assert line["config"]["bytes_per_gpu"] == TCP1500_BYTES
+    assert line["roofline"]["algo_bytes_per_launch"] == TCP1500_BYTES
+    # the PMC traffic is per launch and within a few % of the algorithmic bytes
+    assert 1.0 <= line["roofline"]["traffic"] / TCP1500_BYTES < 1.05
+    cb = line["cpu_baseline"]
+    assert cb["kind"] in ("reference", "port") and cb["cores"] >= 1
+    assert cb["unit"] == "GB/s" and cb["value"] > 0 and cb["sample"]
+
+
+def test_committed_trace_matches_bench_line():
+    with open(os.path.join(PROF, "r01_bench_tcp1500.json")) as f:
+        line = json.loads(f.read().strip().splitlines()[-1])
+    with open(os.path.join(PROF, "r01_tcp1500_kernel_stats.csv")) as f:
+        rows = {r["Name"]: r for r in csv.DictReader(f)}
+    ks = rows["k_stream"]
+    # 50 warm-ups + 200 timed launches + 1 verification launch of the same command
+    assert int(ks["Calls"]) == 251
+    avg_ms = float(ks["AverageNs"]) * 1e-6
+    assert avg_ms == pytest.approx(line["roofline"]["kernel_ms"], rel=0.03)
+
+
+@pytest.mark.gpu
+def test_bench_short_run_prints_contract_line():
+    env = dict(os.environ)
+    out = subprocess.run(
+        [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2",
+         "--no-cpu-baseline"],
+        cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    check_line(line, steps=5, warmup=2)
+    assert line["config"]["bytes_per_gpu"] == TCP1500_BYTES
+    assert line["roofline"]["frac"] > 0.5
