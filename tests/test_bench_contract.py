@@ -32,7 +32,8 @@ def check_line(line: dict, steps: int, warmup: int):
     assert line["scaling"] == "weak" and line["vs_baseline"] is None
     assert line["dtype"] == "u16"
     assert "workload" in line["config"] and "model" not in line["config"]
-    assert line["verified_bit_exact"] is True
+    # bench.py checks the sampled outputs against the reference in its cpu_baseline leg
+    assert line["verified_bit_exact"] is (True if line.get("cpu_baseline") else None)
     r = line["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=2e-3)
