@@ -384,8 +384,13 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
     if (!c || (n && (!base || !d || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
     const uint8_t* b = (const uint8_t*)base;
-    for (uint32_t q = 0; q < n; ++q)
-        if (d[q].offset + (d[q].len > 0 ? (uint64_t)d[q].len : 0u) > base_bytes) return LVLIP_EINVAL;
+    for (uint32_t q = 0; q < n; ++q) {
+        const uint64_t e = d[q].offset + (d[q].len > 0 ? (uint64_t)d[q].len : 0u);
+        if (e > base_bytes) return LVLIP_EINVAL;
+        // a single packet whose 16-B span exceeds the arena: refuse before any
+        // piece is in flight (a piece still in flight would later write into out[])
+        if (align16(e) - (d[q].offset & ~15ull) > c->arena) return LVLIP_ERANGE;
+    }
     DeviceGuard g(c->device);
     const Region* reg = c->regions.empty() ? nullptr : find_region(c, b, base_bytes);
     if (reg && (reg->flags & LVLIP_REG_ZEROCOPY))
@@ -410,10 +415,7 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
             const uint64_t e = o + (d[i].len > 0 ? (uint64_t)d[i].len : 0);
             const uint64_t nlo = (o & ~15ull) < lo16 ? (o & ~15ull) : lo16;
             const uint64_t nhi = e > hi ? e : hi;
-            if (align16(nhi) - nlo > c->arena) {
-                if (k == 0) return LVLIP_ERANGE;
-                break;
-            }
+            if (align16(nhi) - nlo > c->arena) break;  // k >= 1: single spans fit (checked above)
             lo16 = nlo;
             hi = nhi;
             ++k;

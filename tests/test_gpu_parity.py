@@ -562,3 +562,33 @@ def test_max_batch_descriptor_count():
             assert bad == 0, (variant, lo, bad)
     del descs, out, base, dt, tt
     torch.cuda.empty_cache()
+
+
+def test_host_flat_oversized_packet_leaves_nothing_in_flight():
+    """A flat host batch with one packet wider than the context arena is refused
+    with LVLIP_ERANGE before any piece is launched: no earlier piece is left in
+    flight to land in the failed call's out[] during the next call (the
+    contract in INTEGRATION.md §3: a failed batch writes nothing)."""
+    import ctypes
+
+    L = lvlip.lib()
+    arena = 256 << 10
+    n_small = 4000  # ~6 pieces of 100-B packets before the oversized one
+    stride = 112
+    big = arena  # 16-B span arena + 16 > arena
+    base = np.random.default_rng(5).integers(0, 256, n_small * stride + big + 64, dtype=np.uint8)
+    d = np.zeros(n_small + 1, dtype=lvlip.DESC_DTYPE)
+    d["offset"][:n_small] = np.arange(n_small) * stride
+    d["len"][:n_small] = 100
+    d["offset"][n_small] = n_small * stride + 8
+    d["len"][n_small] = big
+    with lvlip.Context(0, arena_bytes=arena) as ctx:
+        bad_out = np.full(n_small + 1, 0xA5A5, dtype=np.uint16)
+        rc = L.lvlip_csum_batch_host_flat(ctx._h, base.ctypes.data, ctypes.c_size_t(base.size),
+                                          d.ctypes.data, n_small + 1, bad_out.ctypes.data)
+        assert rc == lvlip.ERANGE
+        # the next call on the same context is exact, and the failed call's out[]
+        # is still untouched afterwards
+        good = ctx.batch_host_flat(base, d[:n_small])
+        assert np.array_equal(good, pyoracle.batch(base, d[:n_small], threads=THREADS))
+        assert (bad_out == 0xA5A5).all()
