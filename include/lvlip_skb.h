@@ -54,7 +54,8 @@ typedef struct lvlip_frame {
 #define LVLIP_RX_VERIFY_L4   0x1u
 
 /* Verdict per frame; frames are not modified.  Must run before ip_init_pkt's
- * in-place byte swaps (src/ip_input.c:47).  Returns 0 or LVLIP_E*. */
+ * in-place byte swaps (src/ip_input.c:47).  n <= LVLIP_MAX_BATCH / 2 (up to two
+ * checksums per frame).  Returns 0 or LVLIP_E*. */
 int lvlip_rx_verify(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n,
                     uint32_t flags, uint8_t *verdict);
 
@@ -81,7 +82,8 @@ void lvlip_rx_apply(uint32_t n, uint8_t *verdict, uint32_t m, const uint32_t *ta
  *   ICMP : checksum(icmp, ip.len - ihl*4, 0), src/icmpv4.c:46-47
  *   IPv4 : checksum(ih, ihl*4, 0), src/ip_output.c:42,53 (ip_send_check)
  * The IPv4 header checksum does not cover the L4 bytes, so all 2n checksums
- * are one batch.  Returns 0 or LVLIP_E* (frames untouched on error). */
+ * are one batch; n <= LVLIP_MAX_BATCH / 2.  Returns 0 or LVLIP_E* (frames
+ * untouched on error). */
 int lvlip_tx_checksum(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n);
 
 /* Plan: fills iov[]/field[] (capacity 2n; field = where each result goes),

@@ -238,7 +238,8 @@ static void rx_apply_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
 int lvlip_rx_verify(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n, uint32_t flags,
                     uint8_t *verdict)
 {
-    if (!ctx || (n && (!frames || !verdict))) return LVLIP_EINVAL;
+    /* two checksums per frame at most: 2n must fit one batch (as the _dev call) */
+    if (!ctx || (n && (!frames || !verdict)) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
     rx_par a;
     memset(&a, 0, sizeof a);
@@ -379,7 +380,7 @@ static void tx_apply_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
 
 int lvlip_tx_checksum(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n)
 {
-    if (!ctx || (n && !frames)) return LVLIP_EINVAL;
+    if (!ctx || (n && !frames) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
     tx_par a;
     memset(&a, 0, sizeof a);

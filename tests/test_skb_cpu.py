@@ -329,3 +329,20 @@ def test_icmp_incremental_refuses_non_requests():
     with pytest.raises(ValueError):
         lvlip.icmp_echo_reply_fill(fr)
     assert [bytes(f) for f in fr] == before
+
+
+def test_frame_calls_refuse_oversized_batches():
+    """A frame yields up to two checksums, so the host frame calls take at most
+    LVLIP_MAX_BATCH / 2 frames, like the _dev calls (skb_dev.hip): larger n is
+    LVLIP_EINVAL before the context, the frames or any allocation are touched
+    (the dummy pointers below are never dereferenced)."""
+    L = lvlip.lib()
+    dummy = ctypes.create_string_buffer(64)
+    p = ctypes.cast(dummy, ctypes.c_void_p)
+    fp = ctypes.cast(dummy, ctypes.POINTER(lvlip.Frame))
+    too_many = 0xFFFFFFF0 // 2 + 1
+    assert L.lvlip_rx_verify(p, fp, too_many, 0, p) == lvlip.EINVAL
+    assert L.lvlip_tx_checksum(p, fp, too_many) == lvlip.EINVAL
+    # NULL context: EINVAL too, for any n
+    assert L.lvlip_rx_verify(None, fp, 1, 0, p) == lvlip.EINVAL
+    assert L.lvlip_tx_checksum(None, fp, 1) == lvlip.EINVAL
