@@ -251,9 +251,20 @@ def batch_torch(base, descs, out=None, kernel: int = KERNEL_AUTO, unroll: int = 
 
     if not (base.is_cuda and descs.is_cuda):
         raise ValueError("batch_torch needs CUDA tensors")
-    n = descs.numel() * descs.element_size() // 16
+    if descs.device != base.device:
+        raise ValueError("base and descs must be on the same device")
+    if not (base.is_contiguous() and descs.is_contiguous()):
+        raise ValueError("base and descs must be contiguous")
+    nbytes = descs.numel() * descs.element_size()
+    if nbytes % 16:
+        raise ValueError(f"descs holds {nbytes} B, not a multiple of the 16-B descriptor")
+    n = nbytes // 16
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=base.device)
+    elif (not out.is_cuda or out.device != base.device or out.element_size() != 2
+          or not out.is_contiguous() or out.numel() < n):
+        raise ValueError(f"out must be a contiguous 2-byte CUDA tensor of >= {n} elements "
+                         "on base's device")
     if stream is None:
         stream = torch.cuda.current_stream(base.device)
     batch_dev(base.data_ptr(), descs.data_ptr(), n, out.data_ptr(), stream.cuda_stream,

@@ -592,3 +592,23 @@ def test_host_flat_oversized_packet_leaves_nothing_in_flight():
         good = ctx.batch_host_flat(base, d[:n_small])
         assert np.array_equal(good, pyoracle.batch(base, d[:n_small], threads=THREADS))
         assert (bad_out == 0xA5A5).all()
+
+
+def test_batch_torch_rejects_bad_tensors():
+    """The Python mirror refuses tensors whose shape the launch would not match,
+    before anything is launched."""
+    base = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    d = mk_descs([0, 100], [100, 50], [0, 0])
+    descs = dev_descs(d)
+    want = pyoracle.batch(np.zeros(4096, dtype=np.uint8), d)
+    assert np.array_equal(run(base, descs, (lvlip.KERNEL_AUTO, 0, 0)), want)
+    with pytest.raises(ValueError):
+        lvlip.batch_torch(base, descs[:24])  # not a whole descriptor
+    with pytest.raises(ValueError):
+        lvlip.batch_torch(base, descs, torch.empty(1, dtype=torch.int16, device="cuda"))
+    with pytest.raises(ValueError):
+        lvlip.batch_torch(base, descs, torch.empty(2, dtype=torch.int32, device="cuda"))
+    with pytest.raises(ValueError):
+        lvlip.batch_torch(base, descs, torch.empty(4, dtype=torch.int16, device="cuda")[::2])
+    with pytest.raises(ValueError):
+        lvlip.batch_torch(base, descs.cpu())
