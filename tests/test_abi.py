@@ -95,3 +95,13 @@ def test_gfx950_code_object_present():
     blob = open(lvlip.LIB_PATH, "rb").read()
     targets = set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx\w+)", blob))
     assert targets == {b"gfx950"}, targets
+
+
+def test_integration_index_names_every_declared_function():
+    """INTEGRATION.md §6 maps each entry point to the level-ip interface it
+    replaces; a function added to include/*.h without a row there fails here."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    index = doc.split("## 6. Entry-point index", 1)[1]
+    missing = [f for f in declared_functions() if f"`{f}`" not in index]
+    assert not missing, missing
