@@ -47,15 +47,25 @@ def check_line(line: dict, steps: int, warmup: int):
     assert line["value"] <= r["achieved"] * 1.01
 
 
-def test_committed_bench_line_consistent():
-    with open(os.path.join(PROF, "r01_bench_tcp1500.json")) as f:
+# committed line -> (algorithmic bytes per launch, bound on PMC traffic / algorithmic)
+COMMITTED = {
+    "r01_bench_tcp1500.json": (TCP1500_BYTES, 1.05),
+    "r01_bench_tcp9000.json": (1_048_576 * 9000, 1.05),
+    "r01_bench_mixed.json": (1_639_948_630, 1.15),  # layout + descriptors, DESIGN.md §5
+}
+
+
+@pytest.mark.parametrize("name", sorted(COMMITTED))
+def test_committed_bench_line_consistent(name):
+    algo, max_ratio = COMMITTED[name]
+    with open(os.path.join(PROF, name)) as f:
         line = json.loads(f.read().strip().splitlines()[-1])
     check_line(line, steps=200, warmup=50)
     assert line["n_gpus"] == 1
-    assert line["config"]["bytes_per_gpu"] == TCP1500_BYTES
-    assert line["roofline"]["algo_bytes_per_launch"] == TCP1500_BYTES
+    assert line["config"]["bytes_per_gpu"] == algo
+    assert line["roofline"]["algo_bytes_per_launch"] == algo
     # the PMC traffic is per launch and within a few % of the algorithmic bytes
-    assert 1.0 <= line["roofline"]["traffic"] / TCP1500_BYTES < 1.05
+    assert 1.0 <= line["roofline"]["traffic"] / algo < max_ratio
     cb = line["cpu_baseline"]
     assert cb["kind"] in ("reference", "port") and cb["cores"] >= 1
     assert cb["unit"] == "GB/s" and cb["value"] > 0 and cb["sample"]
