@@ -12,6 +12,10 @@ segments).  Prints ONE JSON line (rank 0):
   cpu_baseline  the reference's own checksum() (oracle/_ref, -O0 as its Makefile builds
               it) on the host cores, over a bounded sample of the same packets (rank 0, N=1)
 
+Before the W warm-up steps every rank runs untimed steps for --settle-ms of wall
+time (default 250 ms), so the timed region starts at the GPU's sustained clocks
+rather than in its ramp from idle (diag.settle).
+
 Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`;
 each rank checksums its own shard (packets rank*n .. rank*n+n-1 of the stream:
 weak scaling, no collective on the data path); RCCL is used only for the
@@ -51,10 +55,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--settle-ms", type=float, default=250.0,
+                   help="untimed steps before the warm-up until this much wall time has "
+                        "passed (GPU clock ramp from idle; 0 disables)")
     p.add_argument("--workload", default="tcp1500", choices=sorted(WORKLOAD_TEXT))
     p.add_argument("--n", type=int, default=None, help="packets (frames for mixed) per rank")
     p.add_argument("--kernel", default="auto",
-                   choices=["auto", "wave", "wave_lds", "flat", "wave_simple", "flat_v1"])
+                   choices=["auto", "wave", "wave_lds", "flat", "wave_simple", "flat_v1", "window"])
     p.add_argument("--unroll", type=int, default=0)
     p.add_argument("--waves-per-cu", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -74,9 +81,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def traffic_from_profiles(workload: str, kernel_label: str):
+# the device function each --kernel choice runs (what the PMC records name)
+KERNEL_FN = {"window": "k_window", "wave": "k_stream", "flat": "k_flat2"}
+
+
+def traffic_from_profiles(workload: str, kernel_label: str, kernel_fn: str):
     """HBM bytes per launch measured by rocprofv3 PMC (profiles/*pmc*.json, see
-    profiles/README.md), or None when no matching measurement is committed."""
+    profiles/README.md) for this workload, launch label and device function (the
+    newest file wins), or None when no matching measurement is committed."""
     pdir = os.path.join(ROOT, "profiles")
     best = None
     if not os.path.isdir(pdir):
@@ -90,7 +102,8 @@ def traffic_from_profiles(workload: str, kernel_label: str):
         except (OSError, ValueError):
             continue
         for r in rec.get("kernels", []):
-            if r.get("workload") == workload and r.get("kernel") == kernel_label:
+            if (r.get("workload") == workload and r.get("kernel") == kernel_label
+                    and r.get("kernel_regex") == kernel_fn):
                 best = r.get("hbm_bytes_per_launch")
     return best
 
@@ -248,6 +261,17 @@ def main():
         lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(), stream.cuda_stream,
                         kernel, args.unroll, args.waves_per_cu, len_hint)
 
+    # Bring the GPU to its sustained clocks before the W warm-up steps: from idle,
+    # the first ~15 ms of launches run 5-25 % slow (scripts/warm_curve.py,
+    # DESIGN.md §5), which a 5+20-step run would otherwise time.  Untimed, and
+    # reported in diag.settle.
+    settle_n, ts = 0, time.perf_counter()
+    while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
+        for _ in range(8):
+            step()
+        settle_n += 8
+        torch.cuda.synchronize(dev)
+    settle_ms = (time.perf_counter() - ts) * 1e3
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -279,11 +303,15 @@ def main():
     value = total_bytes * args.steps / wall_max / 1e9
     achieved = b.algo_bytes / (kern_ms / 1e3) / 1e9  # rank 0's kernel, algorithmic bytes
     kernel_label = f"{args.kernel}-u{args.unroll}-w{args.waves_per_cu}"
-    chosen = ({lvlip.KERNEL_WAVE: "wave", lvlip.KERNEL_FLAT: "flat"}[
-        lvlip.KERNEL_WAVE if len_hint >= 512 else lvlip.KERNEL_FLAT]
-        if kernel == lvlip.KERNEL_AUTO else args.kernel)
+    # AUTO's choice (dispatch_one in csum_kernels.hip): contiguous streams for
+    # >= 4 GiB of jumbo packets, the interleaved stream from 512 B, the flat
+    # sweep below
+    chosen = args.kernel
+    if kernel == lvlip.KERNEL_AUTO:
+        jumbo = len_hint >= 4096 and b.n * len_hint >= (4 << 30)
+        chosen = "wave" if jumbo else ("window" if len_hint >= 512 else "flat")
 
-    diag = {}
+    diag = {"settle": {"launches": settle_n, "ms": round(settle_ms, 1)}}
     if scatter_diag is not None:
         diag["scatter"] = scatter_diag
     if rank == 0 and args.sweep:
@@ -317,7 +345,8 @@ def main():
                        "len_hint": len_hint, "parallelism": f"shard{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic_from_profiles(args.workload, kernel_label),
+                         "traffic": traffic_from_profiles(args.workload, kernel_label,
+                                                          KERNEL_FN.get(chosen, "")),
                          "kernel_ms": round(kern_ms, 5),
                          "algo_bytes_per_launch": b.algo_bytes},
             "cpu_baseline": cpu,

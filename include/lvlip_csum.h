@@ -120,7 +120,8 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
                          uint32_t n, uint16_t *out, void *stream);
 
 /* Kernel selection for lvlip_csum_batch_dev_ex.  AUTO picks by len_hint:
- * >= 512 B -> WAVE (8 waves/CU from 4 KiB up, else 16), otherwise or unknown ->
+ * >= 4096 B with n * len_hint >= 4 GiB -> WAVE (2 pieces, 8 waves/CU);
+ * >= 512 B -> WINDOW (shape by the hint); otherwise or unknown ->
  * FLAT (measured: DESIGN.md §5). */
 #define LVLIP_KERNEL_AUTO        0  /* the default                                 */
 #define LVLIP_KERNEL_WAVE        1  /* one wavefront per packet, persistent stream */
@@ -129,10 +130,16 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
 #define LVLIP_KERNEL_WAVE_SIMPLE 4  /* one wave per packet, one launch wave each   */
 #define LVLIP_KERNEL_WAVE_STATIC 6  /* WAVE with a static split only (A/B)        */
 #define LVLIP_KERNEL_WAVE_DYN    7  /* WAVE with a dynamic cross-XCD tail (A/B)   */
+#define LVLIP_KERNEL_WINDOW      8  /* WAVE with packets dealt in small groups
+                                       round robin over the grid (one narrow
+                                       window of the batch in flight)          */
 
 typedef struct lvlip_launch_cfg {
     int32_t  kernel;        /* LVLIP_KERNEL_*                               */
-    int32_t  unroll;        /* 16-B loads in flight per lane (0 = default)  */
+    int32_t  unroll;        /* 16-B loads in flight per lane (0 = default);
+                               WAVE, WINDOW: 2-KiB pieces in flight per
+                               wave; WINDOW: | packets per group << 8
+                               (1, 2, 3, 4 or 8; 0 = by len_hint)           */
     int32_t  waves_per_cu;  /* WAVE: resident waves per CU (0 = 8); others:
                                grid cap (0 = one wave per packet)           */
     int32_t  len_hint;      /* average packet length in bytes if the caller

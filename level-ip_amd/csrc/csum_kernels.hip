@@ -920,6 +920,207 @@ __global__ __launch_bounds__(DYN ? 320 : 256) void k_stream(const uint8_t* __res
     }
 }
 
+// ------------------------------------- k_window (the interleaved stream path) --
+//
+// k_stream's ring, metadata and reduction, with a different deal of packets to
+// waves.  k_stream gives each wave one contiguous range, so the nw waves in
+// flight read nw streams spread over the whole batch.  Here the packets are
+// dealt in groups of G round robin over the grid: the wave of rank r owns
+// groups r, r + nw, r + 2 nw, ... (group j = packets [jG, jG + G)), and its
+// k-th packet is
+//
+//   gidx(k) = ((k / G) * nw + r) * G + k % G.
+//
+// The waves in flight then read one narrow window of the batch (nw x G packets,
+// ~6-9 MB for MTU packets) that slides through it.  Plain streaming reads in that
+// order run 3-6 % faster on MI355X than in nw far-apart streams
+// (scripts/lab_window.py).
+//
+// Everything else is local to the wave's packet sequence k = 0 .. cnt-1: the
+// descriptor windows hold the wave's packets 64k .. 64k+63 (the LDS-DMA takes a
+// per-lane address, so the gather costs nothing extra), and each window's 64
+// results leave as one store with per-lane addresses.
+//
+// Ranks are XCD-major when the grid is a multiple of 8 blocks (block b runs on
+// XCD b % 8 as observed; placement is a speed matter only, every rank is owned
+// by exactly one wave whatever the placement): neighbouring groups then belong
+// to waves of one XCD, so the partial 32-B sectors of their 2-B results merge in
+// that XCD's L2 before they are written back.
+template <int G>
+__device__ __forceinline__ uint64_t window_gidx(uint32_t k, uint64_t nw, uint64_t rank) {
+    return ((uint64_t)(k / G) * nw + rank) * G + (k % G);
+}
+
+template <int G>
+__device__ __forceinline__ void fetch_window_il(const lvlip_csum_desc* __restrict__ descs,
+                                                uint32_t first, uint32_t cnt, uint64_t nw,
+                                                uint64_t rank, uint32_t lane,
+                                                uint4* win /* LDS, 64 entries */) {
+    uint32_t k = first + lane;
+    k = k < cnt ? k : cnt - 1u;  // lanes past the wave's packets re-read a valid descriptor
+    const lvlip_csum_desc* g = descs + window_gidx<G>(k, nw, rank);
+    const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)win);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :
+                 : "v"(g), "s"(lds)
+                 : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
+template <int R, int G>
+__global__ __launch_bounds__(256) void k_window(const uint8_t* __restrict__ base,
+                                                const lvlip_csum_desc* __restrict__ descs,
+                                                uint32_t n, uint16_t* __restrict__ out) {
+    __shared__ uint4 s_win[SW_WAVES][2][64];
+    constexpr uint32_t END = 0xffffffffu;
+    constexpr uint32_t PIECE = 2048u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lane16 = lane * 16u;
+    const uint32_t wid = uniform(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * SW_WAVES;
+    const uint64_t rank =
+        (gridDim.x & 7u) == 0u
+            ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * SW_WAVES + wid
+            : (uint64_t)blockIdx.x * SW_WAVES + wid;
+    // this wave's packets: gcount groups, the last one short when it is the batch's last
+    const uint64_t ng = ((uint64_t)n + G - 1) / G;
+    if (rank >= ng) return;
+    const uint64_t gcount = (ng - 1 - rank) / nw + 1;
+    const uint64_t glast = rank + (gcount - 1) * nw;
+    const uint64_t last_size = min<uint64_t>((uint64_t)G, (uint64_t)n - glast * G);
+    const uint32_t cnt = (uint32_t)((gcount - 1) * G + last_size);
+
+    fetch_window_il<G>(descs, 0u, cnt, nw, rank, lane, s_win[wid][0]);
+    fetch_window_il<G>(descs, 64u, cnt, nw, rank, lane, s_win[wid][1]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    uint32_t m_x, m_y, m_z, m_t, m_s;  // metadata of packet (window + lane), as k_stream
+    auto load_window_meta = [&](uint32_t w) {
+        const uint4 d = s_win[wid][w & 1u][lane];
+        const PacketMeta pm = packet_meta(base, u32x4{d.x, d.y, d.z, d.w});
+        m_x = pm.srd.x;
+        m_y = pm.srd.y;
+        m_z = pm.srd.z;
+        m_t = pm.tinfo;
+        m_s = pm.start;
+    };
+    load_window_meta(0);
+
+    uint32_t ip = 0, io = 0;  // issue cursor: the wave's packet ip, byte offset io in it
+    u32x4 srd;
+    uint32_t tinfo, start;
+    auto pull = [&](uint32_t k) {
+        srd.x = (uint32_t)__builtin_amdgcn_readlane((int)m_x, (int)k);
+        srd.y = (uint32_t)__builtin_amdgcn_readlane((int)m_y, (int)k);
+        srd.z = (uint32_t)__builtin_amdgcn_readlane((int)m_z, (int)k);
+        srd.w = SRD_WORD3;
+        tinfo = (uint32_t)__builtin_amdgcn_readlane((int)m_t, (int)k);
+        start = (uint32_t)__builtin_amdgcn_readlane((int)m_s, (int)k);
+    };
+    pull(0);
+
+    uint32_t gc = 0;  // consume side: results of the wave's packets [gc, gc+64) gather in lanes
+    uint32_t res_w = 0, res_s = 0;
+    uint32_t acc = 0;
+    u32x4 va[R], vb[R];
+    // per piece: the wave's packet index (END past its packets), start_sum, and
+    // meta = last | (len & 3) << 1 | (byte offset of the last dword in the piece) << 3
+    uint32_t s_pkt[R], s_start[R], s_meta[R];
+
+    auto issue = [&](int r) {
+        const bool live = ip < cnt;  // uniform
+        u32x4 sr = srd;
+        if (!live) sr.z = 0;
+        const uint32_t off = lane16 + io;
+        va[r] = buffer_load_nt_asm<0>(off, sr);
+        vb[r] = buffer_load_nt_asm<0>(off + 1024u, sr);
+        const bool last = io + PIECE >= srd.z;
+        s_pkt[r] = live ? ip : END;
+        s_start[r] = start;
+        s_meta[r] = (uint32_t)last | ((tinfo & 3u) << 1) | (((srd.z - 4u) - io) << 3);
+        if (live) {
+            if (!last) {
+                io += PIECE;
+            } else {
+                ++ip;
+                io = 0;
+                if (ip < cnt) {
+                    if ((ip & 63u) == 0u) {  // entered window ip/64
+                        load_window_meta(ip >> 6);
+                        fetch_window_il<G>(descs, ip + 64u, cnt, nw, rank, lane,
+                                           s_win[wid][((ip >> 6) + 1u) & 1u]);
+                    }
+                    pull(ip & 63u);
+                }
+            }
+        }
+    };
+
+    auto consume = [&](int r) {
+        piece_wait<2 * (R - 1)>(va[r], vb[r]);
+        u32x4 x = va[r], y = vb[r];
+        const uint32_t meta = s_meta[r];
+        const uint32_t len3 = (meta >> 1) & 3u;
+        if ((meta & 1u) && len3) {  // uniform: keep bytes [0, len & 3) of the last dword
+            const uint32_t pos = meta >> 3;
+            const uint32_t m = (1u << (8u * len3)) - 1u;
+            const bool me = lane == ((pos >> 4) & 63u);
+            const uint32_t tk = (pos >> 2) & 3u;
+            const bool in_b = pos >= 1024u;
+            const uint32_t m0 = (me && tk == 0u) ? m : ~0u, m1 = (me && tk == 1u) ? m : ~0u;
+            const uint32_t m2 = (me && tk == 2u) ? m : ~0u, m3 = (me && tk == 3u) ? m : ~0u;
+            if (in_b) {
+                y.x &= m0; y.y &= m1; y.z &= m2; y.w &= m3;
+            } else {
+                x.x &= m0; x.y &= m1; x.z &= m2; x.w &= m3;
+            }
+        }
+        acc = dot2_acc(x.x, acc);
+        acc = dot2_acc(x.y, acc);
+        acc = dot2_acc(x.z, acc);
+        acc = dot2_acc(x.w, acc);
+        acc = dot2_acc(y.x, acc);
+        acc = dot2_acc(y.y, acc);
+        acc = dot2_acc(y.z, acc);
+        acc = dot2_acc(y.w, acc);
+        if (meta & 1u) {
+            const uint32_t w = wave_sum_dpp(acc);
+            acc = 0;
+            const uint32_t k = s_pkt[r] - gc;
+            if (lane == k) {
+                res_w = w;
+                res_s = s_start[r];
+            }
+            if (k == 63u || s_pkt[r] + 1u == cnt) {
+                uint32_t tt = res_s + res_w;  // src/utils.c:46-54, per lane
+                tt = (tt & 0xffffu) + (tt >> 16);
+                tt = (tt & 0xffffu) + (tt >> 16);
+                if (lane <= k) out[window_gidx<G>(gc + lane, nw, rank)] = (uint16_t)~tt;
+                gc += 64u;
+            }
+        }
+    };
+
+#pragma unroll
+    for (int r = 0; r < R; ++r) issue(r);
+    bool done = false;
+    while (!done) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (s_pkt[r] == END) {
+                done = true;
+                break;
+            }
+            consume(r);
+            issue(r);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ------------------------------------------------- k_wave_lds (LDS-DMA path) --
 
 template <int U, bool ODD>
@@ -1680,6 +1881,51 @@ bool launch_stream_dyn(int waves_per_cu, hipStream_t s, const void* base,
     return true;
 }
 
+// k_window: waves_per_cu waves on every CU (fewer when the batch has fewer
+// groups), R pieces in flight per wave, groups of G packets.  The grid stays a
+// multiple of 8 blocks when it can, so the ranks are XCD-major.
+template <int R, int G>
+void launch_window_g(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                     uint32_t n, uint16_t* out) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    uint64_t waves = (uint64_t)cu_count(dev) * (uint64_t)waves_per_cu;
+    const uint64_t ng = ((uint64_t)n + G - 1) / G;
+    if (waves > ng) waves = ng;
+    uint64_t grid = (waves + lvlip::SW_WAVES - 1) / lvlip::SW_WAVES;
+    if (grid > 8) grid = grid & ~7ull;
+    hipLaunchKernelGGL((lvlip::k_window<R, G>), dim3((uint32_t)grid), dim3(256), 0, s,
+                       (const uint8_t*)base, d, n, out);
+}
+
+// Packets per group: the caller's (cfg->unroll >> 8), else LVLIP_WINDOW_GROUP
+// (A/B knob, read once), else by the length hint.
+int window_group(int requested, int len_hint) {
+    static const int v = [] {
+        const char* e = getenv("LVLIP_WINDOW_GROUP");
+        return e ? atoi(e) : 0;
+    }();
+    if (requested == 1 || requested == 2 || requested == 3 || requested == 4 || requested == 8)
+        return requested;
+    if (v == 1 || v == 2 || v == 3 || v == 4 || v == 8) return v;
+    if (len_hint <= 0) return 4;
+    if (len_hint >= 3072) return 1;
+    if (len_hint >= 1280) return 4;
+    return 8;
+}
+
+template <int R>
+void launch_window(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                   uint32_t n, uint16_t* out, int group, int len_hint) {
+    switch (window_group(group, len_hint)) {
+        case 1: launch_window_g<R, 1>(waves_per_cu, s, base, d, n, out); break;
+        case 3: launch_window_g<R, 3>(waves_per_cu, s, base, d, n, out); break;
+        case 4: launch_window_g<R, 4>(waves_per_cu, s, base, d, n, out); break;
+        case 8: launch_window_g<R, 8>(waves_per_cu, s, base, d, n, out); break;
+        default: launch_window_g<R, 2>(waves_per_cu, s, base, d, n, out); break;
+    }
+}
+
 template <int U>
 void launch_wave_lds(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
                      uint32_t n, uint16_t* out) {
@@ -1728,14 +1974,19 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         // MTU/jumbo segments, the flat sweep on mixed header/payload batches and
         // stays within ~10 % elsewhere, so it is the choice when sizes are unknown.
         const int hint = cfg ? cfg->len_hint : 0;
-        if (hint >= 512) {
-            // shapes from scripts/shape_sweep.py: MTU-sized
-            // packets run best at 8 waves/CU with 3 in flight per wave
-            // (~36 KiB per CU), jumbo at 8 waves with 2 pieces, the rest at 16
+        if (hint >= 4096 && (uint64_t)n * (uint64_t)hint >= (4ull << 30)) {
+            // jumbo batches of >= 4 GiB: contiguous per-wave ranges stream
+            // 0.6 % faster than the interleaved deal (tcp9000)
             kernel = LVLIP_KERNEL_WAVE;
-            const bool mtu = hint >= 1280 && hint < 2048;
-            if (wpc <= 0) wpc = (hint >= 4096 || mtu) ? 8 : 16;
-            if (unroll <= 0 && mtu) unroll = 3;
+            if (wpc <= 0) wpc = 8;
+            if (unroll <= 0) unroll = 2;
+        } else if (hint >= 512) {
+            // the interleaved stream, shapes from scripts/shape_sweep.py
+            // (DESIGN.md §4): 2 pieces in flight per wave; groups of ~4-6 KB;
+            // more waves per CU for smaller packets (per-packet work)
+            kernel = LVLIP_KERNEL_WINDOW;
+            if (wpc <= 0) wpc = hint < 1280 ? 16 : (hint < 2048 ? 12 : 8);
+            if (unroll <= 0) unroll = 2 | ((hint < 2048 ? 4 : (hint < 4096 ? 2 : 1)) << 8);
         } else {
             kernel = LVLIP_KERNEL_FLAT;
         }
@@ -1768,6 +2019,22 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
                     if (!dyn || !launch_stream_dyn<4>(w, s, base, descs, n, out, hint, xd))
                         launch_stream<4>(w, s, base, descs, n, out, fb);
                     break;
+                default: return LVLIP_EINVAL;
+            }
+            break;
+        }
+        case LVLIP_KERNEL_WINDOW: {
+            // unroll = 2-KiB pieces in flight per wave (low byte, default 3) |
+            // packets per group << 8 (0 = by len_hint); 8 waves/CU by default
+            const int group = unroll > 0 ? (unroll >> 8) & 0xff : 0;
+            int r = unroll > 0 ? unroll & 0xff : 0;
+            if (r == 0) r = 3;
+            const int w = wpc > 0 ? wpc : 8;
+            const int hint = cfg ? cfg->len_hint : 0;
+            switch (r) {
+                case 2: launch_window<2>(w, s, base, descs, n, out, group, hint); break;
+                case 3: launch_window<3>(w, s, base, descs, n, out, group, hint); break;
+                case 4: launch_window<4>(w, s, base, descs, n, out, group, hint); break;
                 default: return LVLIP_EINVAL;
             }
             break;

@@ -75,6 +75,22 @@ __global__ __launch_bounds__(256) void k_probe(const uint4* __restrict__ src, ui
             for (int u = 0; u < U; ++u) acc += words(v[2 * u]) + (part ? words(v[2 * u + 1]) : 0u);
         }
         for (; p < hi; ++p) acc += words(ld<NT>(src + p * 94 + lane));
+    } else if (MODE == 5) {
+        // chip-wide window: chunk c = U consecutive 1 KiB pieces; wave w reads chunks
+        // w, w + nw, w + 2 nw, ... so the waves in flight cover one narrow sliding
+        // window of the buffer instead of nw far-apart streams
+        const uint64_t pieces = n16 / 64;
+        const uint64_t nw = (uint64_t)gridDim.x * wpb;
+        const uint64_t chunks = pieces / U;
+        for (uint64_t c = (uint64_t)blockIdx.x * wpb + wid; c < chunks; c += nw) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ld<NT>(src + (c * U + u) * 64 + lane);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += words(v[u]);
+        }
+        for (uint64_t p = chunks * U + (uint64_t)blockIdx.x * wpb + wid; p < pieces; p += nw)
+            acc += words(ld<NT>(src + p * 64 + lane));
     } else {
         const uint64_t pieces = n16 / 64;  // 1 KiB pieces
         uint64_t lo, hi, step, first;
@@ -101,6 +117,68 @@ __global__ __launch_bounds__(256) void k_probe(const uint4* __restrict__ src, ui
             for (int u = 0; u < U; ++u) acc += words(v[u]);
         }
         for (; p < hi; p += step) acc += words(ld<NT>(src + p * 64 + lane));
+    }
+    acc = wsum(acc);
+    if (lane == 0) atomicAdd(sink, acc);
+}
+
+// Chip-wide window with the chunk size decoupled from the depth: a chunk is
+// `cp` consecutive 1 KiB pieces (cp a multiple of U); wave w owns chunks
+// w, w + nw, ... and walks each one U pieces (U KiB in flight) at a time.
+// The window the waves in flight cover is nw * cp KiB.
+// order 1 numbers the waves XCD-major (block b sits on XCD b % 8 as observed;
+// grid a multiple of 8), so consecutive chunks stay on one XCD.
+template <int U>
+__global__ __launch_bounds__(256) void k_probe_chunk(const uint4* __restrict__ src, uint64_t n16,
+                                                     uint32_t cp, uint32_t order,
+                                                     uint32_t* __restrict__ sink) {
+    uint32_t acc = 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint64_t pieces = n16 / 64;
+    const uint64_t nw = (uint64_t)gridDim.x * wpb;
+    const uint64_t chunks = pieces / cp;
+    const uint64_t rank = order ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * wpb + wid
+                                : (uint64_t)blockIdx.x * wpb + wid;
+    for (uint64_t c = rank; c < chunks; c += nw) {
+        for (uint32_t q = 0; q < cp; q += U) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ld<true>(src + (c * cp + q + u) * 64 + lane);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += words(v[u]);
+        }
+    }
+    for (uint64_t p = chunks * cp + (uint64_t)blockIdx.x * wpb + wid; p < pieces; p += nw)
+        acc += words(ld<true>(src + p * 64 + lane));
+    acc = wsum(acc);
+    if (lane == 0) atomicAdd(sink, acc);
+}
+
+// Packetized chip-wide window: 1504-B slots (tcp1500's layout) in groups of G;
+// wave rank r (XCD-major) reads groups r, r + nw, ...; per group all 2G loads
+// (one full 1 KiB + one 30-lane load per slot) are issued, then summed.
+template <int G>
+__global__ __launch_bounds__(256) void k_probe_pkwin(const uint4* __restrict__ src, uint64_t n16,
+                                                     uint32_t* __restrict__ sink) {
+    uint32_t acc = 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint64_t nw = (uint64_t)gridDim.x * 4u;
+    const uint64_t rank = ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * 4u + wid;
+    const uint64_t groups = n16 / 94 / G;
+    const bool part = lane < 30u;
+    for (uint64_t g = rank; g < groups; g += nw) {
+        uint4 v[2 * G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const uint64_t p = g * G + u;
+            v[2 * u] = ld<true>(src + p * 94 + lane);
+            v[2 * u + 1] = ld<true>(src + p * 94 + 64 + (part ? lane : 29u));
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) acc += words(v[2 * u]) + (part ? words(v[2 * u + 1]) : 0u);
     }
     acc = wsum(acc);
     if (lane == 0) atomicAdd(sink, acc);
@@ -235,6 +313,7 @@ extern "C" int lvlip_lab_probe(const void* src, uint64_t bytes, uint32_t* sink, 
     CASES(1, 1) CASES(1, 2) CASES(1, 4) CASES(1, 8)
     CASES(2, 1) CASES(2, 2) CASES(2, 4) CASES(2, 8)
     CASES(4, 1) CASES(4, 2) CASES(4, 3) CASES(4, 4)
+    CASES(5, 1) CASES(5, 2) CASES(5, 4) CASES(5, 8)
 #undef CASES
 #undef CASE
     if (mode == 3) {
@@ -245,6 +324,34 @@ extern "C" int lvlip_lab_probe(const void* src, uint64_t bytes, uint32_t* sink, 
         else return -1;
         return hipGetLastError() == hipSuccess ? 0 : -3;
     }
+    return -1;
+}
+
+extern "C" int lvlip_lab_probe_chunk(const void* src, uint64_t bytes, uint32_t* sink, int unroll,
+                                     uint32_t chunk_pieces, uint32_t order, int blocks, void* stream) {
+    if (!src || !sink || (bytes & 1023u) || chunk_pieces == 0 || chunk_pieces % (uint32_t)unroll ||
+        (order && (blocks & 7)))
+        return -1;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 g((uint32_t)blocks), b(256);
+    const uint64_t n16 = bytes / 16;
+#define CH(U) \
+    if (unroll == U) { hipLaunchKernelGGL(k_probe_chunk<U>, g, b, 0, s, (const uint4*)src, n16, chunk_pieces, order, sink); return hipGetLastError() == hipSuccess ? 0 : -3; }
+    CH(2) CH(3) CH(4) CH(6) CH(8)
+#undef CH
+    return -1;
+}
+
+extern "C" int lvlip_lab_probe_pkwin(const void* src, uint64_t bytes, uint32_t* sink, int group,
+                                     int blocks, void* stream) {
+    if (!src || !sink || (bytes & 15u) || (blocks & 7)) return -1;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 g((uint32_t)blocks), b(256);
+    const uint64_t n16 = bytes / 16;
+#define PW(G) \
+    if (group == G) { hipLaunchKernelGGL(k_probe_pkwin<G>, g, b, 0, s, (const uint4*)src, n16, sink); return hipGetLastError() == hipSuccess ? 0 : -3; }
+    PW(1) PW(2) PW(3) PW(4) PW(6) PW(8)
+#undef PW
     return -1;
 }
 

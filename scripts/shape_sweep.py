@@ -5,7 +5,8 @@ batches of L-byte packets (16-B aligned slots, ~1.5 GB), times every
 process.  The table behind AUTO's choice in dispatch_one (csum_kernels.hip).
 
 env: SH_LENS (default 512,768,1024,1500,2048,3000,4096,9000),
-     SH_SHAPES (default 2x8,2x16,3x8,3x12,4x8,4x16), SH_ROUNDS (2)
+     SH_SHAPES (default 2x8,2x16,3x8,3x12,4x8,4x16), SH_ROUNDS (2),
+     SH_WINDOW (k_window shapes RxWxG: pieces in flight, waves/CU, packets per group)
 writes JSON to argv[1]."""
 import json
 import os
@@ -56,13 +57,18 @@ def main():
         algo = n * L + 2 * n
         row = res.setdefault(str(L), {})
         variants = [("auto", 0, 0)] + [("wave", r, w) for r, w in shapes]
+        # k_window shapes: SH_WINDOW = RxWxG,... (pieces in flight, waves/CU, group)
+        for sh in filter(None, os.environ.get("SH_WINDOW", "").split(",")):
+            r, w, gsz = (int(v) for v in sh.split("x"))
+            variants.append(("window", r | (gsz << 8), w))
         for _ in range(rounds):
             for k, r, w in variants:
                 def f():
                     lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), n, out.data_ptr(), s.cuda_stream,
                                     lvlip.KERNEL_NAMES[k], r, w, L)
                 ms = timed(f, s)
-                row.setdefault(f"{k}-{r}x{w}", []).append(round(algo / ms / 1e6, 1))
+                key = f"{k}-{r & 0xff}x{w}" + (f"g{r >> 8}" if r >> 8 else "")
+                row.setdefault(key, []).append(round(algo / ms / 1e6, 1))
         best = max(row, key=lambda k: max(row[k]))
         print(f"L={L:5d} n={n:8d} " + "  ".join(f"{k}:{max(v):7.1f}" for k, v in row.items()) + f"  best {best}",
               flush=True)

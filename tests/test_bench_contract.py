@@ -1,6 +1,6 @@
 """The bench line's contract, checked two ways.
 
-* CPU: the committed evidence (`profiles/r01_bench_tcp1500.json` and the rocprof
+* CPU: the committed evidence (`profiles/r02_bench_<workload>.json` and the rocprof
   summary of the same command) is self-consistent -- the fields the driver and
   the judge read are present, `value`/`roofline` follow from the byte count and
   the timings, and the trace's average k_stream duration agrees with the line's
@@ -49,10 +49,12 @@ def check_line(line: dict, steps: int, warmup: int):
 
 # committed line -> (algorithmic bytes per launch, bound on PMC traffic / algorithmic)
 COMMITTED = {
-    "r01_bench_tcp1500.json": (TCP1500_BYTES, 1.05),
-    "r01_bench_tcp9000.json": (1_048_576 * 9000, 1.05),
-    "r01_bench_mixed.json": (1_639_948_630, 1.15),  # layout + descriptors, DESIGN.md §5
+    "r02_bench_tcp1500.json": (TCP1500_BYTES, 1.05),
+    "r02_bench_tcp9000.json": (1_048_576 * 9000, 1.05),
+    "r02_bench_mixed.json": (1_639_948_630, 1.15),  # layout + descriptors, DESIGN.md §5
 }
+# the device function AUTO runs for each committed line (bench.py KERNEL_FN)
+DOMINANT = {"tcp1500": "k_window", "tcp9000": "k_stream", "mixed": "k_flat2"}
 
 
 @pytest.mark.parametrize("name", sorted(COMMITTED))
@@ -65,20 +67,30 @@ def test_committed_bench_line_consistent(name):
     assert line["config"]["bytes_per_gpu"] == algo
     assert line["roofline"]["algo_bytes_per_launch"] == algo
     # the PMC traffic is per launch and within a few % of the algorithmic bytes
-    assert 1.0 <= line["roofline"]["traffic"] / algo < max_ratio
+    # (committed beside the line; the line itself carries it once that file exists)
+    wl = name[len("r02_bench_"):-len(".json")]
+    with open(os.path.join(PROF, f"r02_pmc_{wl}.json")) as f:
+        pmc = json.load(f)["kernels"][0]
+    assert pmc["kernel_regex"] == DOMINANT[wl] and pmc["algo_bytes_per_launch"] == algo
+    assert 1.0 <= pmc["hbm_bytes_per_launch"] / algo < max_ratio
+    if line["roofline"]["traffic"] is not None:
+        assert 1.0 <= line["roofline"]["traffic"] / algo < max_ratio
+    assert line["diag"]["settle"]["ms"] >= 200  # clock settle before the warm-up
     cb = line["cpu_baseline"]
     assert cb["kind"] in ("reference", "port") and cb["cores"] >= 1
     assert cb["unit"] == "GB/s" and cb["value"] > 0 and cb["sample"]
 
 
-def test_committed_trace_matches_bench_line():
-    with open(os.path.join(PROF, "r01_bench_tcp1500.json")) as f:
+@pytest.mark.parametrize("wl", sorted(DOMINANT))
+def test_committed_trace_matches_bench_line(wl):
+    with open(os.path.join(PROF, f"r02_bench_{wl}.json")) as f:
         line = json.loads(f.read().strip().splitlines()[-1])
-    with open(os.path.join(PROF, "r01_tcp1500_kernel_stats.csv")) as f:
+    with open(os.path.join(PROF, f"r02_{wl}_kernel_stats.csv")) as f:
         rows = {r["Name"]: r for r in csv.DictReader(f)}
-    ks = rows["k_stream"]
-    # 50 warm-ups + 200 timed launches + 1 verification launch of the same command
-    assert int(ks["Calls"]) == 251
+    ks = rows[DOMINANT[wl]]
+    # the clock-settle launches (~1 000, their count varies with the run) + 50
+    # warm-ups + 200 timed launches + 1 verification launch of the same command
+    assert int(ks["Calls"]) >= 251 + 8
     avg_ms = float(ks["AverageNs"]) * 1e-6
     assert avg_ms == pytest.approx(line["roofline"]["kernel_ms"], rel=0.03)
 

@@ -41,6 +41,9 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT, 2, 0),
     (lvlip.KERNEL_FLAT, 8, 0),
     (5, 0, 0),                     # first-generation flat kernel (A/B)
+    (lvlip.KERNEL_WINDOW, 3, 0),   # interleaved stream: groups dealt round robin
+    (lvlip.KERNEL_WINDOW, 2, 1),   # 1 wave/CU: long per-wave sequences, window refills
+    (lvlip.KERNEL_WINDOW, 4, 24),
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
@@ -211,6 +214,7 @@ def test_full_size_bit_exact(name):
     assert bad.size == 0, f"{bad.size} of {b.n} differ; first {bad[:5]}"
     # size-independent property: every kernel variant agrees, and reruns are identical
     for variant in [(lvlip.KERNEL_WAVE, 4, 0), (lvlip.KERNEL_WAVE, 3, 4),
+                    (lvlip.KERNEL_WINDOW, 3, 0), (lvlip.KERNEL_WINDOW, 2, 0),
                     (lvlip.KERNEL_WAVE_DYN, 2, 0), (lvlip.KERNEL_WAVE_DYN, 2, 8),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
@@ -222,6 +226,37 @@ def test_full_size_bit_exact(name):
     assert ones.any() and zeros.any()
     del base, descs, out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("group", [0, 1, 2, 3, 4, 8])
+def test_window_groups(group):
+    """k_window for every group size, on batch sizes that leave the last group
+    short, give some waves no packets, or several windows per wave; mixed
+    lengths (odd, empty, 64 KiB) at odd offsets; every output against the oracle."""
+    rng = np.random.default_rng(group)
+    n_max = 70000
+    ln = rng.integers(0, 3000, n_max).astype(np.int32)
+    ln[rng.random(n_max) < 0.01] = 0
+    ln[rng.random(n_max) < 0.001] = 65535
+    ln[rng.random(n_max) < 0.01] = -3
+    off = np.zeros(n_max, dtype=np.uint64)
+    off[1:] = np.cumsum(np.maximum(ln, 0)[:-1] + rng.integers(0, 19, n_max - 1))
+    off += 5
+    blob = rng.integers(0, 256, int(off[-1]) + max(int(ln[-1]), 0) + 64, dtype=np.uint8)
+    st = rng.integers(0, 2**32, n_max, dtype=np.uint64).astype(np.uint32)
+    d = mk_descs(off, ln, st)
+    want = pyoracle.batch(blob, d, threads=THREADS)
+    base = dev_blob(blob)
+    for n in (1, 2, 3, 7, 63, 64, 65, 129, 2047, 2048 * 2 + 1, 33333, n_max):
+        descs = dev_descs(d[:n])
+        for unroll, wpc in ((2, 0), (3, 0), (4, 0), (3, 1), (2, 24)):
+            # unroll = pieces in flight | packets per group << 8 (0: by the hint)
+            out = lvlip.batch_torch(base, descs, kernel=lvlip.KERNEL_WINDOW,
+                                    unroll=unroll | (group << 8), waves_per_cu=wpc, len_hint=1500)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().view(np.uint16)
+            bad = np.nonzero(got != want[:n])[0]
+            assert bad.size == 0, (n, unroll, wpc, bad[:5])
 
 
 def test_config5_96gb_chunked():

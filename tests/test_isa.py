@@ -1,6 +1,7 @@
-"""ISA guards for the stream kernel (CPU-only: hipcc cross-compiles gfx950).
+"""ISA guards for the stream kernels (CPU-only: hipcc cross-compiles gfx950).
 
-The stream kernel relies on hand-placed inline asm (csum_kernels.hip, k_stream):
+The stream kernels rely on hand-placed inline asm (csum_kernels.hip, k_stream and
+k_window, which shares its ring):
   * buffer_load_dwordx4 whose resource words come from v_readfirstlane, a VALU
     write of SGPRs: a VMEM read of them needs 5 wait states (s_nop 4), which
     hipcc does not insert around inline asm;
@@ -70,12 +71,22 @@ def is_fb(name):
 
 
 def stream_kernels(asm):
+    """k_stream and k_window instantiations (the ring kernels)."""
     f = functions(asm)
-    ks = {n: body for n, body in f.items() if "k_stream" in n}
-    assert ks, "no k_stream instantiations found"
+    ks = {n: body for n, body in f.items() if "k_stream" in n or "k_window" in n}
+    assert any("k_stream" in n for n in ks), "no k_stream instantiations found"
     assert any(is_dyn(n) for n in ks), "no k_stream<.., DYN = true> instantiations found"
     assert any(is_fb(n) for n in ks), "no k_stream<.., FB = true> instantiations found"
+    # k_window<R, G>: every pieces-in-flight x group-size pair the launcher uses
+    win = {tuple(int(x) for x in re.search(r"k_windowILi(\d+)ELi(\d+)E", n).groups())
+           for n in ks if "k_window" in n}
+    assert win == {(r, g) for r in (2, 3, 4) for g in (1, 2, 3, 4, 8)}, sorted(win)
     return ks
+
+
+def pieces(name):
+    """R (pieces in flight) of a k_stream / k_window instantiation."""
+    return int(re.search(r"k_(?:stream|window)ILi(\d+)E", name).group(1))
 
 
 def test_buffer_loads_padded_against_valu_sgpr_hazard(asm):
@@ -107,7 +118,7 @@ def test_ring_waits_are_counted_not_draining(asm):
     for name, body in stream_kernels(asm).items():
         if is_dyn(name):
             continue  # test_dyn_streamers_never_drain
-        r = int(re.search(r"k_streamILi(\d+)E", name).group(1))  # pieces in flight
+        r = pieces(name)
         waits = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt" in ins]
         ring = [w for w in waits if f"vmcnt({2 * (r - 1)})" in w]
         assert len(ring) == r, (name, waits)
@@ -125,7 +136,7 @@ def test_ring_waits_are_counted_not_draining(asm):
 
 
 def test_no_scratch(asm):
-    for m in re.finditer(r"\.name:\s+(_Z\w*k_stream\w*)\n(?:.*\n){0,60}?\s+\.private_segment_fixed_size:\s+(\d+)",
+    for m in re.finditer(r"\.name:\s+(_Z\w*k_(?:stream|window)\w*)\n(?:.*\n){0,60}?\s+\.private_segment_fixed_size:\s+(\d+)",
                          asm):
         assert int(m.group(2)) == 0, m.group(1)
 
@@ -138,7 +149,7 @@ def test_dyn_streamers_never_drain(asm):
     for name, body in stream_kernels(asm).items():
         if not is_dyn(name):
             continue
-        r = int(re.search(r"k_streamILi(\d+)E", name).group(1))
+        r = pieces(name)
         waits = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt" in ins]
         assert sum(f"vmcnt({2 * (r - 1)})" in w for w in waits) >= r, (name, waits)
         other = 0
