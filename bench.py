@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--workload", default="tcp1500", choices=sorted(WORKLOAD_TEXT))
     p.add_argument("--n", type=int, default=None, help="packets (frames for mixed) per rank")
     p.add_argument("--kernel", default="auto",
-                   choices=["auto", "wave", "wave_lds", "flat", "wave_simple", "flat_v1", "window"])
+                   choices=["auto", "wave", "wave_lds", "flat", "wave_simple", "flat_v1", "window", "wflat"])
     p.add_argument("--unroll", type=int, default=0)
     p.add_argument("--waves-per-cu", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -82,7 +82,7 @@ def log(*a):
 
 
 # the device function each --kernel choice runs (what the PMC records name)
-KERNEL_FN = {"window": "k_window", "wave": "k_stream", "flat": "k_flat2"}
+KERNEL_FN = {"window": "k_window", "wave": "k_stream", "flat": "k_flat2", "wflat": "k_wflat"}
 
 
 def traffic_from_profiles(workload: str, kernel_label: str, kernel_fn: str):

@@ -133,13 +133,17 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
 #define LVLIP_KERNEL_WINDOW      8  /* WAVE with packets dealt in small groups
                                        round robin over the grid (one narrow
                                        window of the batch in flight)          */
+#define LVLIP_KERNEL_WFLAT       9  /* FLAT's chunk sweep, one wave per tile of
+                                       descriptors, tiles dealt round robin    */
 
 typedef struct lvlip_launch_cfg {
     int32_t  kernel;        /* LVLIP_KERNEL_*                               */
     int32_t  unroll;        /* 16-B loads in flight per lane (0 = default);
                                WAVE, WINDOW: 2-KiB pieces in flight per
                                wave; WINDOW: | packets per group << 8
-                               (1, 2, 3, 4 or 8; 0 = by len_hint)           */
+                               (1, 2, 3, 4 or 8; 0 = by len_hint);
+                               WFLAT: 64-chunk loads per round | descriptors
+                               per tile << 8 (16, 32 or 64; 0 = 32)          */
     int32_t  waves_per_cu;  /* WAVE: resident waves per CU (0 = 8); others:
                                grid cap (0 = one wave per packet)           */
     int32_t  len_hint;      /* average packet length in bytes if the caller

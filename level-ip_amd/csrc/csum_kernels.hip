@@ -1597,6 +1597,274 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
     }
     src.put(i_me, res, ctx, i_me < n, a0 + lo);
 }
+
+// ------------------------------------------- k_wflat (ragged, window deal) --
+//
+// k_flat2's chunk sweep, one wave per tile of D descriptors, with the tiles
+// dealt round robin over the grid as k_window deals its packet groups: wave
+// rank r (XCD-major) sweeps tiles r, r + nw, r + 2 nw, ...  A k_flat2 workgroup
+// owns 256 descriptors (~100 KB of a mixed batch) and its four waves sweep
+// contiguous quarters of them, so the waves in flight read ~8 000 streams over
+// ~200 MB; here the waves in flight read one window of nw x D descriptors
+// (~13-25 MB of a mixed batch) that slides through the batch.  The read probes
+// on the mixed buffer measure that order 4.7 % faster (scripts/lab_window.py,
+// DESIGN.md §4).
+//
+// Per tile, all in one wave (no workgroup barrier):
+//   1. lane i < D reads descriptor i; chunk counts, an exclusive wave scan of
+//      them (the tile's virtual chunk space), a rank among the non-empty small
+//      descriptors (mbcnt of a ballot), records by rank and a head bitmap per
+//      64-chunk load in the wave's LDS;
+//   2. the sweep: U loads of 64 chunks per round, every lane's packet found as
+//      in k_flat2 (heads before the load + mbcnt), bytes outside the packet
+//      masked in the lane (its first and last chunk), odd-address packets
+//      byte-swapped, and segment sums by the inclusive-scan trick into the
+//      descriptor's LDS accumulator;
+//   3. descriptors longer than WCAP chunks: one wave-per-packet loop each;
+//   4. fold, ~, one store of the tile's D results.
+constexpr uint32_t WCAP = 128;  // chunks of the largest swept descriptor (2 KiB)
+
+template <int D>
+struct WflatLds {
+    uint4 rec[SW_WAVES][D];                 // by rank: {a0 lo, a0 hi, cstart, meta}
+    uint2 msk[SW_WAVES][D * WCAP / 64];     // head bitmap per 64-chunk load
+    uint32_t acc[SW_WAVES][D];              // by descriptor
+    uint4 edge[SW_WAVES][2 * D];            // by descriptor: raw first / last chunk
+};
+
+// Orders this wave's LDS traffic across lanes (a lane reading what another
+// lane wrote): LDS ops of one wave execute in order, so the compiler only has
+// to be kept from moving them, and the counter drained.  No vmcnt: global
+// loads in flight stay in flight.
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int U, int D>
+__global__ __launch_bounds__(256) void k_wflat(const uint8_t* __restrict__ base,
+                                               const lvlip_csum_desc* __restrict__ descs,
+                                               uint32_t n, uint16_t* __restrict__ out) {
+    static_assert(D >= 1 && D <= 64, "one descriptor per lane");
+    __shared__ WflatLds<D> L;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = uniform(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * SW_WAVES;
+    const uint64_t rank =
+        (gridDim.x & 7u) == 0u
+            ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * SW_WAVES + wid
+            : (uint64_t)blockIdx.x * SW_WAVES + wid;
+    const uint64_t ntiles = ((uint64_t)n + D - 1) / D;
+    uint4* s_rec = L.rec[wid];
+    uint2* s_msk = L.msk[wid];
+    uint32_t* s_acc = L.acc[wid];
+    uint4* s_edge = L.edge[wid];
+
+    // descriptors of the wave's next tile, one 16-B load per lane issued a tile
+    // ahead (lanes past the batch re-read its last descriptor)
+    // Issued from asm, so hipcc's wait-count pass does not see it in flight and
+    // drain it before the sweep's first loads; the sweep's own waits retire it
+    // (vector memory ops retire in issue order), and the loop head waits for it
+    // explicitly, which costs nothing after a tile that had a sweep round.
+    auto fetch = [&](uint64_t t, u32x4& d) {
+        uint64_t i = t * D + (lane < (uint32_t)D ? lane : 0u);
+        i = i < n ? i : n - 1u;
+        const lvlip_csum_desc* g = descs + i;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(g) : "memory");
+    };
+    u32x4 dnext;
+    fetch(rank < ntiles ? rank : 0u, dnext);
+    // the previous tile's results, stored once the next prefetch is retired
+    uint64_t i_prev = 0;
+    bool st_prev = false;
+    uint16_t res_prev = 0;
+    for (uint64_t t = rank; t < ntiles; t += nw) {
+        const uint64_t i = t * D + lane;
+        const bool mine = lane < (uint32_t)D && i < n;
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(dnext) : : "memory");
+        const u32x4 dv = dnext;  // {offset lo, offset hi, len, start_sum}
+        // the previous tile's store and the next tile's prefetch go out behind
+        // this tile's first sweep loads, so they share their round trip (the
+        // store's data register is reused soon after, and the wait hipcc puts
+        // before that reuse drains everything in flight)
+        bool side_done = false;
+        auto side = [&]() {
+            if (st_prev) out[i_prev] = res_prev;
+            st_prev = false;
+            if (t + nw < ntiles) fetch(t + nw, dnext);
+            side_done = true;
+        };
+        // ---- 1. descriptors -> chunk space, records, head bitmap
+        uint32_t start_sum = 0, nch = 0, meta = 0;
+        uint64_t a0 = 0;
+        bool big = false;
+        if (mine) {
+            lvlip_csum_desc d;
+            d.offset = ((uint64_t)dv.y << 32) | dv.x;
+            d.len = (int32_t)dv.z;
+            d.start_sum = dv.w;
+            start_sum = d.start_sum;
+            if (d.len > 0) {
+                const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
+                a0 = abs & ~15ull;
+                const uint32_t lo = (uint32_t)(abs & 15ull);
+                const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
+                const uint64_t c64 = (span + 15u) >> 4;
+                const uint32_t lastv = (uint32_t)(span - 16ull * (c64 - 1u));  // 1..16
+                big = c64 > WCAP;
+                nch = big ? 0u : (uint32_t)c64;
+                // edge flags: the sweep stashes the first (bit 24) and last (bit
+                // 25) chunk in LDS when they hold bytes outside the descriptor,
+                // and step 4 subtracts those bytes (as k_flat2)
+                const bool ef = !big && (lo != 0u || (c64 == 1u && lastv != 16u));
+                const bool el = !big && c64 > 1u && lastv != 16u;
+                // meta: nch (8 bits) | lo << 8 | lastv << 12 | odd << 17 | lane << 18 | ef, el
+                meta = nch | (lo << 8) | (lastv << 12) | ((uint32_t)(abs & 1ull) << 17) | (lane << 18) |
+                       ((uint32_t)ef << 24) | ((uint32_t)el << 25);
+            }
+        }
+        const uint32_t incl = wave_incl_scan(nch);
+        const uint32_t C = uniform((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
+        const uint32_t cstart = incl - nch;
+        const uint64_t nz = __builtin_amdgcn_ballot_w64(nch != 0u);
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
+        const uint32_t nloads = (C + 63u) >> 6;
+        for (uint32_t q = lane; q < nloads; q += 64u) s_msk[q] = make_uint2(0u, 0u);
+        if (lane < (uint32_t)D) s_acc[lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (nch) {
+            s_rec[r] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), cstart, meta);
+            const uint32_t q = cstart >> 6, b = cstart & 63u;
+            if (b < 32u) atomicOr(&s_msk[q].x, 1u << b);
+            else atomicOr(&s_msk[q].y, 1u << (b - 32u));
+        }
+        lds_sync();
+
+        // ---- 2. sweep the tile's chunk space, U loads of 64 chunks per round
+        uint32_t heads = 0;  // heads in the loads before this round
+        for (uint32_t u0 = 0; u0 < nloads; u0 += U) {
+            uint32_t hb[U], hlo[U], hhi[U];
+            bool gv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                gv[u] = u0 + u < nloads;
+                const uint2 m = s_msk[gv[u] ? u0 + u : nloads - 1u];
+                hlo[u] = uniform(m.x);
+                hhi[u] = uniform(m.y);
+                hb[u] = heads;
+                heads += gv[u] ? (uint32_t)__popcll(((uint64_t)hhi[u] << 32) | hlo[u]) : 0u;
+            }
+            uint4 x[U], rec[U];
+            uint32_t kk[U];
+            bool vl[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = (u0 + u) * 64u + lane;
+                vl[u] = gv[u] && c < C;
+                const uint64_t H = ((uint64_t)hhi[u] << 32) | hlo[u];
+                const uint64_t Hs = H >> 1;
+                const uint32_t cnt = __builtin_amdgcn_mbcnt_hi((uint32_t)(Hs >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)Hs, 0u));
+                // a valid chunk's packet: heads at or below it - 1 (chunk 0 is a
+                // head); lanes past the chunk space read record 0's first chunk,
+                // a valid address, and are zeroed
+                const uint32_t rk = hb[u] + (uint32_t)(H & 1ull) + cnt - 1u;
+                rec[u] = s_rec[vl[u] ? rk : 0u];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = (u0 + u) * 64u + lane;
+                kk[u] = vl[u] ? c - rec[u].z : 0u;
+                const uint64_t ca = (((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * kk[u];
+                x[u] = load_nt_global(ca);
+            }
+            if (!side_done) side();
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!gv[u]) break;  // uniform
+                uint4 v = x[u];
+                const uint32_t m = rec[u].w;
+                const uint32_t pn = m & 0xFFu;
+                const bool first = kk[u] == 0u;
+                const bool last = kk[u] + 1u == pn;
+                const uint32_t q = (m >> 18) & 63u;
+                if (vl[u] && first && (m & (1u << 24))) s_edge[2u * q] = x[u];
+                if (vl[u] && last && (m & (1u << 25))) s_edge[2u * q + 1u] = x[u];
+                if (__builtin_amdgcn_ballot_w64((m & (1u << 17)) != 0u)) {
+                    const uint32_t sel = (m & (1u << 17)) ? 0x02030001u : 0x03020100u;
+                    v.x = __builtin_amdgcn_perm(v.x, v.x, sel);
+                    v.y = __builtin_amdgcn_perm(v.y, v.y, sel);
+                    v.z = __builtin_amdgcn_perm(v.z, v.z, sel);
+                    v.w = __builtin_amdgcn_perm(v.w, v.w, sel);
+                }
+                uint32_t val = 0;
+                val = dot2_acc(v.x, val);
+                val = dot2_acc(v.y, val);
+                val = dot2_acc(v.z, val);
+                val = dot2_acc(v.w, val);
+                val = vl[u] ? val : 0u;
+                const uint32_t P = wave_incl_scan(val);
+                const uint32_t add = (first ? val - P : 0u) + ((last || lane == 63u) ? P : 0u);
+                if (vl[u] && (first || last || lane == 63u)) atomicAdd(&s_acc[q], add);
+            }
+        }
+
+        if (!side_done) side();  // a tile with nothing to sweep
+
+        // ---- 3. descriptors longer than WCAP chunks, one wave each
+        uint64_t bigm = __builtin_amdgcn_ballot_w64(big);
+        while (bigm) {
+            const uint32_t q = (uint32_t)__builtin_ctzll(bigm);
+            bigm &= bigm - 1ull;
+            const lvlip_csum_desc d = descs[t * D + q];
+            const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
+            const int lo = (int)(abs & 15ull);
+            const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
+            const uint32_t nchq = (uint32_t)((span + 15u) >> 4);
+            const uint32_t lastv = (uint32_t)(span - 16ull * (nchq - 1u));
+            const uint4* src = reinterpret_cast<const uint4*>(abs & ~15ull);
+            uint32_t w = (abs & 1ull) ? wave_packet_sum<4, true>(src, nchq, lo, lastv, lane)
+                                      : wave_packet_sum<4, false>(src, nchq, lo, lastv, lane);
+            w = wave_sum_dpp(w);
+            if (lane == 0) s_acc[q] = w;
+        }
+        lds_sync();
+
+        // ---- 4. edge corrections (bytes of the first / last chunk outside the
+        // descriptor, once per descriptor, mod 2^32), fold; the store goes out
+        // behind the next tile's first sweep loads
+        uint32_t acc = s_acc[lane < (uint32_t)D ? lane : 0u];
+        if (meta & (3u << 24)) {
+            const bool odd = meta & (1u << 17);
+            const int lo = (int)((meta >> 8) & 15u), lastv = (int)((meta >> 12) & 31u);
+            uint32_t c = 0;
+            if (meta & (1u << 24)) {
+                uint4 f = s_edge[2u * lane];
+                const int fb1 = (nch == 1u) ? lastv : 16;
+                f.x &= ~byte_range_mask(lo, fb1, 0);
+                f.y &= ~byte_range_mask(lo, fb1, 1);
+                f.z &= ~byte_range_mask(lo, fb1, 2);
+                f.w &= ~byte_range_mask(lo, fb1, 3);
+                c += odd ? chunk_words<true>(f) : chunk_words<false>(f);
+            }
+            if (meta & (1u << 25)) {
+                uint4 l = s_edge[2u * lane + 1u];
+                l.x &= ~byte_range_mask(0, lastv, 0);
+                l.y &= ~byte_range_mask(0, lastv, 1);
+                l.z &= ~byte_range_mask(0, lastv, 2);
+                l.w &= ~byte_range_mask(0, lastv, 3);
+                c += odd ? chunk_words<true>(l) : chunk_words<false>(l);
+            }
+            acc -= c;
+        }
+        res_prev = finish(start_sum, acc);
+        i_prev = i;
+        st_prev = mine;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (st_prev) out[i_prev] = res_prev;
+}
 }  // namespace lvlip
 
 // ======================================================== host side (C ABI) ==
@@ -1679,6 +1947,18 @@ bool flat_contig() {
         return !(e && strcmp(e, "interleaved") == 0);
     }();
     return c;
+}
+
+// LVLIP_FLAT_LDS_PAD (A/B knob, read once): bytes of unused dynamic LDS per
+// k_flat2 workgroup, which caps the resident workgroups per CU (160 KiB / (19 KiB
+// + pad)); 0 = none.
+size_t flat_lds_pad() {
+    static const size_t v = [] {
+        const char* e = getenv("LVLIP_FLAT_LDS_PAD");
+        const long x = e ? atol(e) : 0;
+        return (size_t)(x < 0 ? 0 : (x > 131072 ? 131072 : x));
+    }();
+    return v;
 }
 
 template <int U>
@@ -1926,6 +2206,33 @@ void launch_window(int waves_per_cu, hipStream_t s, const void* base, const lvli
     }
 }
 
+// k_wflat: waves_per_cu waves on every CU (fewer when the batch has fewer
+// tiles); the grid stays a multiple of 8 blocks when it can (XCD-major ranks).
+template <int U, int D>
+void launch_wflat_ud(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                     uint32_t n, uint16_t* out) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    uint64_t waves = (uint64_t)cu_count(dev) * (uint64_t)waves_per_cu;
+    const uint64_t nt = ((uint64_t)n + D - 1) / D;
+    if (waves > nt) waves = nt;
+    uint64_t grid = (waves + lvlip::SW_WAVES - 1) / lvlip::SW_WAVES;
+    if (grid > 8) grid = grid & ~7ull;
+    hipLaunchKernelGGL((lvlip::k_wflat<U, D>), dim3((uint32_t)grid), dim3(256), 0, s,
+                       (const uint8_t*)base, d, n, out);
+}
+
+template <int U>
+bool launch_wflat(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                  uint32_t n, uint16_t* out, int tile) {
+    switch (tile) {
+        case 16: launch_wflat_ud<U, 16>(waves_per_cu, s, base, d, n, out); return true;
+        case 32: launch_wflat_ud<U, 32>(waves_per_cu, s, base, d, n, out); return true;
+        case 64: launch_wflat_ud<U, 64>(waves_per_cu, s, base, d, n, out); return true;
+        default: return false;
+    }
+}
+
 template <int U>
 void launch_wave_lds(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
                      uint32_t n, uint16_t* out) {
@@ -2039,6 +2346,24 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             }
             break;
         }
+        case LVLIP_KERNEL_WFLAT: {
+            // unroll = 64-chunk loads per round (low byte, default 4) | descriptors
+            // per tile << 8 (16, 32 or 64; 0 = 32); 8 waves/CU by default
+            int u = unroll > 0 ? unroll & 0xff : 0;
+            int tile = unroll > 0 ? (unroll >> 8) & 0xff : 0;
+            if (u == 0) u = 4;
+            if (tile == 0) tile = 32;
+            const int w = wpc > 0 ? wpc : 8;
+            bool ok = false;
+            switch (u) {
+                case 2: ok = launch_wflat<2>(w, s, base, descs, n, out, tile); break;
+                case 4: ok = launch_wflat<4>(w, s, base, descs, n, out, tile); break;
+                case 8: ok = launch_wflat<8>(w, s, base, descs, n, out, tile); break;
+                default: break;
+            }
+            if (!ok) return LVLIP_EINVAL;
+            break;
+        }
         case LVLIP_KERNEL_WAVE_SIMPLE: {
             if (unroll <= 0) unroll = 2;
             const uint32_t grid = grid_for(n, 4, wpc, 4);
@@ -2070,7 +2395,7 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
 #define LVLIP_FLAT(UU, NTV, CG)                                                               \
     case UU * 4 + (NTV ? 2 : 0) + (CG ? 1 : 0):                                              \
         hipLaunchKernelGGL((lvlip::k_flat2<UU, NTV, CG, lvlip::DescSrc>), dim3(grid),         \
-                           dim3(lvlip::FT), 0, s, (const uint8_t*)base,                      \
+                           dim3(lvlip::FT), flat_lds_pad(), s, (const uint8_t*)base,         \
                            lvlip::DescSrc{descs, out}, n);                                  \
         break;
                 LVLIP_FLAT(2, true, true) LVLIP_FLAT(2, true, false)

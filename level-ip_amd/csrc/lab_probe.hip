@@ -159,7 +159,9 @@ __global__ __launch_bounds__(256) void k_probe_chunk(const uint4* __restrict__ s
 // Packetized chip-wide window: 1504-B slots (tcp1500's layout) in groups of G;
 // wave rank r (XCD-major) reads groups r, r + nw, ...; per group all 2G loads
 // (one full 1 KiB + one 30-lane load per slot) are issued, then summed.
-template <int G>
+// SPAN: the group's G slots read as one span in whole 1 KiB loads (the last
+// one partial) instead of two loads per slot.
+template <int G, bool SPAN>
 __global__ __launch_bounds__(256) void k_probe_pkwin(const uint4* __restrict__ src, uint64_t n16,
                                                      uint32_t* __restrict__ sink) {
     uint32_t acc = 0;
@@ -169,6 +171,23 @@ __global__ __launch_bounds__(256) void k_probe_pkwin(const uint4* __restrict__ s
     const uint64_t rank = ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * 4u + wid;
     const uint64_t groups = n16 / 94 / G;
     const bool part = lane < 30u;
+    if (SPAN) {
+        constexpr uint32_t NCH = 94u * G;            // chunks of the span
+        constexpr uint32_t NL = (NCH + 63u) / 64u;   // whole loads
+        for (uint64_t g = rank; g < groups; g += nw) {
+            uint4 v[NL];
+#pragma unroll
+            for (uint32_t u = 0; u < NL; ++u) {
+                const uint32_t c = u * 64u + lane;
+                v[u] = ld<true>(src + g * NCH + (c < NCH ? c : NCH - 1u));
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < NL; ++u) acc += (u * 64u + lane < NCH) ? words(v[u]) : 0u;
+        }
+        acc = wsum(acc);
+        if (lane == 0) atomicAdd(sink, acc);
+        return;
+    }
     for (uint64_t g = rank; g < groups; g += nw) {
         uint4 v[2 * G];
 #pragma unroll
@@ -349,7 +368,8 @@ extern "C" int lvlip_lab_probe_pkwin(const void* src, uint64_t bytes, uint32_t* 
     const dim3 g((uint32_t)blocks), b(256);
     const uint64_t n16 = bytes / 16;
 #define PW(G) \
-    if (group == G) { hipLaunchKernelGGL(k_probe_pkwin<G>, g, b, 0, s, (const uint4*)src, n16, sink); return hipGetLastError() == hipSuccess ? 0 : -3; }
+    if (group == G) { hipLaunchKernelGGL((k_probe_pkwin<G, false>), g, b, 0, s, (const uint4*)src, n16, sink); return hipGetLastError() == hipSuccess ? 0 : -3; } \
+    if (group == 100 + G) { hipLaunchKernelGGL((k_probe_pkwin<G, true>), g, b, 0, s, (const uint4*)src, n16, sink); return hipGetLastError() == hipSuccess ? 0 : -3; }
     PW(1) PW(2) PW(3) PW(4) PW(6) PW(8)
 #undef PW
     return -1;

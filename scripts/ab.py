@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""A/B of launch variants on one resident batch (GPU box).
+
+  AB_WORKLOAD=mixed AB_VARIANTS="flat:4:0,flat:8:0,auto:0:0" python scripts/ab.py [out.json]
+
+A variant is kernel:unroll:waves_per_cu[:len_hint] (kernel names as bench.py's
+--kernel; len_hint defaults to the batch's average length).  After a clock
+settle, interleaved rounds in one process (AB_ROUNDS, default 5) each time every
+variant over 20 launches with HIP events; prints the median GB/s of algorithmic
+bytes per variant, and checks that every variant computes the same checksums.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "level-ip_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import lvlip  # noqa: E402
+import workloads  # noqa: E402
+
+
+def timed(fn, stream, reps=20, warm=3):
+    for _ in range(warm):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    out_path = sys.argv[1] if len(sys.argv) > 1 else None
+    wl = os.environ.get("AB_WORKLOAD", "tcp1500")
+    rounds = int(os.environ.get("AB_ROUNDS", "5"))
+    dev = torch.device("cuda", 0)
+    b = workloads.make(wl)
+    base, descs, out = workloads.to_device(b, dev)
+    s = torch.cuda.current_stream(dev)
+    hint = b.algo_bytes // b.n
+    variants = []
+    for v in os.environ.get("AB_VARIANTS", "auto:0:0").split(","):
+        f = v.split(":")
+        variants.append((v, f[0], int(f[1], 0), int(f[2]), int(f[3]) if len(f) > 3 else hint))
+
+    def mk(k, u, w, h):
+        return lambda: lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
+                                       s.cuda_stream, lvlip.KERNEL_NAMES[k], u, w, h)
+    timed(mk("auto", 0, 0, hint), s, reps=400)  # clock settle
+    ref, res = None, {}
+    for rnd in range(rounds):
+        for key, k, u, w, h in variants:
+            ms = timed(mk(k, u, w, h), s)
+            res.setdefault(key, []).append(b.algo_bytes / ms / 1e6)
+            if rnd == 0:
+                got = out.cpu().numpy().copy()
+                ref = got if ref is None else ref
+                assert np.array_equal(got, ref), key
+    summary = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
+    for k, v in sorted(summary.items(), key=lambda kv: -kv[1]):
+        print(f"{wl} {k:24s} {v:8.1f} GB/s   rounds {[round(x) for x in res[k]]}", flush=True)
+    if out_path:
+        with open(out_path, "w") as f:
+            json.dump({"workload": wl, "median_GBps": summary, "rounds": res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -64,8 +64,13 @@ def main():
         for u, cp in ((3, 3), (4, 4), (6, 6)):
             variants.append(("c", u, cp, 0, 3))
         variants += [(2, 8, 0, 0, 2)]
+    elif lab_set == "ragged":
+        # the mixed buffer: window vs contiguous orders at 8 and 32 waves/CU
+        variants += [("c", 4, 4, 1, 2), ("c", 4, 4, 1, 8), ("c", 4, 16, 1, 8), ("c", 8, 8, 1, 4),
+                     (2, 8, 0, 0, 2), (2, 4, 0, 0, 8), (1, 8, 0, 0, 2), (1, 4, 0, 0, 8)]
     elif lab_set == "pkwin":
-        for g in (1, 2, 3, 4, 6, 8):
+        # group g: two loads per slot; 100 + g: the group's span in whole loads
+        for g in (1, 2, 3, 4, 6, 8, 101, 102, 103, 104, 106, 108):
             variants.append(("p", g, 0, 0, 2))
         for g in (2, 3):
             variants.append(("p", g, 0, 0, 3))

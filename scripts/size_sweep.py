@@ -54,12 +54,17 @@ def main():
         row["probe_ms"] = min(timed(lambda: lab.lvlip_lab_probe(base.data_ptr(), nb, sink.data_ptr(), 1, 8, 1,
                                                                  cus * 2, s.cuda_stream), s)
                               for _ in range(3))
+        # the window-order read probe (4 KiB chunks dealt round robin)
+        row["wprobe_ms"] = min(timed(lambda: lab.lvlip_lab_probe_chunk(base.data_ptr(), nb, sink.data_ptr(),
+                                                                       4, 4, 1, cus * 2, s.cuda_stream), s)
+                               for _ in range(3))
         print(json.dumps(row), flush=True)
         rows.append(row)
         del base, descs, out
         torch.cuda.empty_cache()
     fits = {}
-    for key, bytes_key in [(k + "_ms", "algo_bytes") for k in kernels] + [("probe_ms", "probe_bytes")]:
+    for key, bytes_key in [(k + "_ms", "algo_bytes") for k in kernels] + [("probe_ms", "probe_bytes"),
+                                                                              ("wprobe_ms", "probe_bytes")]:
         x = np.array([r[bytes_key] for r in rows], dtype=np.float64)
         y = np.array([r[key] for r in rows], dtype=np.float64)
         slope, icpt = np.polyfit(x, y, 1)

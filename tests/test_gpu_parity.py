@@ -44,6 +44,9 @@ VARIANTS = [
     (lvlip.KERNEL_WINDOW, 3, 0),   # interleaved stream: groups dealt round robin
     (lvlip.KERNEL_WINDOW, 2, 1),   # 1 wave/CU: long per-wave sequences, window refills
     (lvlip.KERNEL_WINDOW, 4, 24),
+    (lvlip.KERNEL_WFLAT, 0, 0),    # flat sweep per wave, tiles dealt round robin
+    (lvlip.KERNEL_WFLAT, 2 | (16 << 8), 1),
+    (lvlip.KERNEL_WFLAT, 8 | (64 << 8), 16),
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
@@ -215,6 +218,7 @@ def test_full_size_bit_exact(name):
     # size-independent property: every kernel variant agrees, and reruns are identical
     for variant in [(lvlip.KERNEL_WAVE, 4, 0), (lvlip.KERNEL_WAVE, 3, 4),
                     (lvlip.KERNEL_WINDOW, 3, 0), (lvlip.KERNEL_WINDOW, 2, 0),
+                    (lvlip.KERNEL_WFLAT, 0, 0), (lvlip.KERNEL_WFLAT, 8 | (64 << 8), 16),
                     (lvlip.KERNEL_WAVE_DYN, 2, 0), (lvlip.KERNEL_WAVE_DYN, 2, 8),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
@@ -228,13 +232,10 @@ def test_full_size_bit_exact(name):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("group", [0, 1, 2, 3, 4, 8])
-def test_window_groups(group):
-    """k_window for every group size, on batch sizes that leave the last group
-    short, give some waves no packets, or several windows per wave; mixed
-    lengths (odd, empty, 64 KiB) at odd offsets; every output against the oracle."""
-    rng = np.random.default_rng(group)
-    n_max = 70000
+def ragged_batch(seed, n_max=70000):
+    """Random lengths 0-3000 B (odd ones, 1 % empty, 1 % negative, 0.1 % 64 KiB)
+    at odd and even offsets with random gaps, and the oracle's checksums."""
+    rng = np.random.default_rng(seed)
     ln = rng.integers(0, 3000, n_max).astype(np.int32)
     ln[rng.random(n_max) < 0.01] = 0
     ln[rng.random(n_max) < 0.001] = 65535
@@ -245,9 +246,19 @@ def test_window_groups(group):
     blob = rng.integers(0, 256, int(off[-1]) + max(int(ln[-1]), 0) + 64, dtype=np.uint8)
     st = rng.integers(0, 2**32, n_max, dtype=np.uint64).astype(np.uint32)
     d = mk_descs(off, ln, st)
-    want = pyoracle.batch(blob, d, threads=THREADS)
-    base = dev_blob(blob)
-    for n in (1, 2, 3, 7, 63, 64, 65, 129, 2047, 2048 * 2 + 1, 33333, n_max):
+    return dev_blob(blob), d, pyoracle.batch(blob, d, threads=THREADS)
+
+
+BATCH_SIZES = (1, 2, 3, 7, 15, 16, 17, 31, 63, 64, 65, 129, 2047, 2048 * 2 + 1, 33333, 70000)
+
+
+@pytest.mark.parametrize("group", [0, 1, 2, 3, 4, 8])
+def test_window_groups(group):
+    """k_window for every group size, on batch sizes that leave the last group
+    short, give some waves no packets, or several windows per wave; mixed
+    lengths (odd, empty, 64 KiB) at odd offsets; every output against the oracle."""
+    base, d, want = ragged_batch(group)
+    for n in BATCH_SIZES:
         descs = dev_descs(d[:n])
         for unroll, wpc in ((2, 0), (3, 0), (4, 0), (3, 1), (2, 24)):
             # unroll = pieces in flight | packets per group << 8 (0: by the hint)
@@ -257,6 +268,23 @@ def test_window_groups(group):
             got = out.cpu().numpy().view(np.uint16)
             bad = np.nonzero(got != want[:n])[0]
             assert bad.size == 0, (n, unroll, wpc, bad[:5])
+
+
+@pytest.mark.parametrize("tile", [0, 16, 32, 64])
+def test_wflat_tiles(tile):
+    """k_wflat for every tile size and depth, on batch sizes that leave the last
+    tile short or give waves no tile, with descriptors past the sweep cap
+    (64 KiB), empty and negative lengths at odd offsets; against the oracle."""
+    base, d, want = ragged_batch(100 + tile)
+    for n in BATCH_SIZES:
+        descs = dev_descs(d[:n])
+        for u, wpc in ((2, 0), (4, 0), (8, 0), (4, 1), (2, 16)):
+            out = lvlip.batch_torch(base, descs, kernel=lvlip.KERNEL_WFLAT, unroll=u | (tile << 8),
+                                    waves_per_cu=wpc)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().view(np.uint16)
+            bad = np.nonzero(got != want[:n])[0]
+            assert bad.size == 0, (n, u, wpc, bad[:5])
 
 
 def test_config5_96gb_chunked():
