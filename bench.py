@@ -59,7 +59,9 @@ def parse():
                    help="untimed steps before the warm-up until this much wall time has "
                         "passed (GPU clock ramp from idle; 0 disables)")
     p.add_argument("--workload", default="tcp1500", choices=sorted(WORKLOAD_TEXT))
-    p.add_argument("--n", type=int, default=None, help="packets (frames for mixed) per rank")
+    p.add_argument("--n", "--packets", dest="n", type=int, default=None,
+                   help="packets (frames for mixed) per rank (--packets under torch.distributed.run, "
+                        "whose own parser takes --n for a prefix of its options)")
     p.add_argument("--kernel", default="auto",
                    choices=["auto", "wave", "wave_lds", "flat", "wave_simple", "flat_v1", "window", "wflat"])
     p.add_argument("--unroll", type=int, default=0)
@@ -264,7 +266,12 @@ def main():
     # Bring the GPU to its sustained clocks before the W warm-up steps: from idle,
     # the first ~15 ms of launches run 5-25 % slow (scripts/warm_curve.py,
     # DESIGN.md §5), which a 5+20-step run would otherwise time.  Untimed, and
-    # reported in diag.settle.
+    # reported in diag.settle.  With N > 1 ranks the first collective (which
+    # sets up the communicator and can take a second) runs before the settle, so
+    # the GPUs do not idle between their settle and the timed region.
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize(dev)
     settle_n, ts = 0, time.perf_counter()
     while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
         for _ in range(8):

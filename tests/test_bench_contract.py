@@ -109,3 +109,27 @@ def test_bench_short_run_prints_contract_line():
     check_line(line, steps=5, warmup=2)
     assert line["config"]["bytes_per_gpu"] == TCP1500_BYTES
     assert line["roofline"]["frac"] > 0.5
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_rehearsal_prints_one_line():
+    """The N>1 path (torch.distributed.run, one process per rank, barriers and
+    the max-over-ranks time) with 2 ranks sharing the box's one GPU over gloo
+    (LVLIP_DIST_BACKEND=gloo): rank 0 prints one line for the whole job."""
+    env = dict(os.environ, LVLIP_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    out = subprocess.run(
+        [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+         "--master-addr", "127.0.0.1", "--master-port", "29531",
+         os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2",
+         "--packets", "262144", "--settle-ms", "50"],
+        cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["steps"] == 5 and line["warmup"] == 2
+    assert line["config"]["bytes_per_gpu"] == 262144 * 1500
+    # whole-job bytes over the slower rank's wall time
+    assert line["value"] == pytest.approx(2 * 262144 * 1500 / (line["ms_per_step"] * 1e-3) / 1e9,
+                                          rel=5e-3)
+    assert line["cpu_baseline"] is None  # rank 0 at N=1 only
