@@ -2388,7 +2388,10 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         }
         case LVLIP_KERNEL_FLAT: {
             const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
-            if (unroll <= 0) unroll = 4;
+            // 8 loads of 64 chunks per round: 94 VGPRs, 5 workgroups per CU with
+            // 8 KiB in flight per wave; 2-3 % ahead of 4 (8 workgroups, 4 KiB)
+            // on mixed in 3 of 4 same-process A/B runs
+            if (unroll <= 0) unroll = 8;
             const bool nt = load_nt();
             const bool contig = flat_contig();
             switch (unroll * 4 + (nt ? 2 : 0) + (contig ? 1 : 0)) {
@@ -2404,6 +2407,7 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
                 LVLIP_FLAT(4, false, true) LVLIP_FLAT(4, false, false)
                 LVLIP_FLAT(8, true, true) LVLIP_FLAT(8, true, false)
                 LVLIP_FLAT(8, false, true) LVLIP_FLAT(8, false, false)
+                LVLIP_FLAT(6, true, true) LVLIP_FLAT(12, true, true)
 #undef LVLIP_FLAT
                 default: return LVLIP_EINVAL;
             }

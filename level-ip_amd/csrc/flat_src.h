@@ -22,9 +22,19 @@ namespace lvlip {
 struct DescSrc {
     const lvlip_csum_desc* descs;
     uint16_t* out;
+    // One 16-B load: read field by field, hipcc splits the descriptor into a
+    // len load and an offset load behind it, two round trips at the start of
+    // every tile.
     __device__ __forceinline__ lvlip_csum_desc get(uint32_t i, uint32_t& ctx) const {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) const v4u gv4u;
         ctx = 0;
-        return descs[i];
+        const v4u v = *reinterpret_cast<gv4u*>(reinterpret_cast<uint64_t>(descs + i));
+        lvlip_csum_desc d;
+        d.offset = ((uint64_t)v.y << 32) | v.x;
+        d.len = (int32_t)v.z;
+        d.start_sum = v.w;
+        return d;
     }
     __device__ __forceinline__ void put(uint32_t i, uint16_t c, uint32_t, bool valid, uint64_t) const {
         if (valid) out[i] = c;

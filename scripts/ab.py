@@ -4,11 +4,14 @@
   AB_WORKLOAD=mixed AB_VARIANTS="flat:4:0,flat:8:0,auto:0:0" python scripts/ab.py [out.json]
 
 A variant is kernel:unroll:waves_per_cu[:len_hint] (kernel names as bench.py's
---kernel; len_hint defaults to the batch's average length).  After a clock
+--kernel; len_hint defaults to the batch's average length).  A variant prefixed
+"alt/" runs through the library AB_ALT_LIB instead (another revision of the
+product, built by scripts/build_ab.sh), so two builds compare in one process.  After a clock
 settle, interleaved rounds in one process (AB_ROUNDS, default 5) each time every
 variant over 20 launches with HIP events; prints the median GB/s of algorithmic
 bytes per variant, and checks that every variant computes the same checksums.
 """
+import ctypes
 import json
 import os
 import sys
@@ -43,12 +46,26 @@ def main():
     base, descs, out = workloads.to_device(b, dev)
     s = torch.cuda.current_stream(dev)
     hint = b.algo_bytes // b.n
+    alt = None
+    if os.environ.get("AB_ALT_LIB"):
+        import ctypes
+        alt = ctypes.CDLL(os.path.abspath(os.environ["AB_ALT_LIB"]))
+        alt.lvlip_csum_batch_dev_ex.restype = ctypes.c_int
+        alt.lvlip_csum_batch_dev_ex.argtypes = lvlip.SIGNATURES["lvlip_csum_batch_dev_ex"][1]
     variants = []
     for v in os.environ.get("AB_VARIANTS", "auto:0:0").split(","):
         f = v.split(":")
         variants.append((v, f[0], int(f[1], 0), int(f[2]), int(f[3]) if len(f) > 3 else hint))
 
     def mk(k, u, w, h):
+        if k.startswith("alt/"):
+            cfg = lvlip.LaunchCfg(lvlip.KERNEL_NAMES[k[4:]], u, w, h)
+
+            def f():
+                rc = alt.lvlip_csum_batch_dev_ex(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
+                                                 s.cuda_stream, ctypes.byref(cfg))
+                assert rc == 0, rc
+            return f
         return lambda: lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
                                        s.cuda_stream, lvlip.KERNEL_NAMES[k], u, w, h)
     timed(mk("auto", 0, 0, hint), s, reps=400)  # clock settle

@@ -40,6 +40,8 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT, 0, 0),
     (lvlip.KERNEL_FLAT, 2, 0),
     (lvlip.KERNEL_FLAT, 8, 0),
+    (lvlip.KERNEL_FLAT, 6, 0),
+    (lvlip.KERNEL_FLAT, 12, 0),
     (5, 0, 0),                     # first-generation flat kernel (A/B)
     (lvlip.KERNEL_WINDOW, 3, 0),   # interleaved stream: groups dealt round robin
     (lvlip.KERNEL_WINDOW, 2, 1),   # 1 wave/CU: long per-wave sequences, window refills
