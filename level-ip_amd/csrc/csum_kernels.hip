@@ -2459,6 +2459,16 @@ int lvlip_csum_batch_dev(const void* base, const lvlip_csum_desc* descs, uint32_
 
 namespace {
 
+// LVLIP_FRAMES_UNROLL (A/B knob, read once): loads per round of the frame
+// calls' sweep, 4 (default) or 8.
+int frames_unroll() {
+    static const int v = [] {
+        const char* e = getenv("LVLIP_FRAMES_UNROLL");
+        return e && atoi(e) == 8 ? 8 : 4;
+    }();
+    return v;
+}
+
 template <int MODE>
 int launch_frames(const void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* out8,
                   hipStream_t s) {
@@ -2470,8 +2480,12 @@ int launch_frames(const void* base, const lvlip_frame_desc* frames, uint32_t n, 
         const uint32_t entries = m * Src::SLOTS;
         const uint32_t grid = (uint32_t)(((uint64_t)entries + lvlip::FT - 1) / lvlip::FT);
         Src src{(const uint8_t*)base, (uint8_t*)base, frames + f0, out8 ? out8 + f0 : nullptr};
-        hipLaunchKernelGGL((lvlip::k_flat2<4, true, true, Src>), dim3(grid), dim3(lvlip::FT), 0, s,
-                           (const uint8_t*)base, src, entries);
+        if (frames_unroll() == 8)
+            hipLaunchKernelGGL((lvlip::k_flat2<8, true, true, Src>), dim3(grid), dim3(lvlip::FT), 0, s,
+                               (const uint8_t*)base, src, entries);
+        else
+            hipLaunchKernelGGL((lvlip::k_flat2<4, true, true, Src>), dim3(grid), dim3(lvlip::FT), 0, s,
+                               (const uint8_t*)base, src, entries);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "k_flat2 (frames)");
         f0 += m;
