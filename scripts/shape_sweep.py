@@ -6,7 +6,8 @@ process.  The table behind AUTO's choice in dispatch_one (csum_kernels.hip).
 
 env: SH_LENS (default 512,768,1024,1500,2048,3000,4096,9000),
      SH_SHAPES (default 2x8,2x16,3x8,3x12,4x8,4x16), SH_ROUNDS (2),
-     SH_WINDOW (k_window shapes RxWxG: pieces in flight, waves/CU, packets per group)
+     SH_WINDOW (k_window shapes RxWxG: pieces in flight, waves/CU, packets per group),
+     SH_TOTAL (bytes of packet slots per length, default 1.5e9)
 writes JSON to argv[1]."""
 import json
 import os
@@ -40,7 +41,7 @@ def main():
     rounds = int(os.environ.get("SH_ROUNDS", "2"))
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream(dev)
-    total = 1_500_000_000
+    total = int(float(os.environ.get("SH_TOTAL", "1.5e9")))  # bytes of packet slots per length
     g = torch.Generator(device=dev)
     g.manual_seed(0x1E7E1C5)
     base = torch.randint(0, 256, (total + 16 * 9008,), dtype=torch.uint8, device=dev, generator=g)
