@@ -310,13 +310,11 @@ def main():
     value = total_bytes * args.steps / wall_max / 1e9
     achieved = b.algo_bytes / (kern_ms / 1e3) / 1e9  # rank 0's kernel, algorithmic bytes
     kernel_label = f"{args.kernel}-u{args.unroll}-w{args.waves_per_cu}"
-    # AUTO's choice (dispatch_one in csum_kernels.hip): contiguous streams for
-    # >= 4 GiB of jumbo packets, the interleaved stream from 512 B, the flat
-    # sweep below
+    # AUTO's choice (dispatch_one in csum_kernels.hip): the interleaved stream
+    # from 512 B, the flat sweep below
     chosen = args.kernel
     if kernel == lvlip.KERNEL_AUTO:
-        jumbo = len_hint >= 4096 and b.n * len_hint >= (4 << 30)
-        chosen = "wave" if jumbo else ("window" if len_hint >= 512 else "flat")
+        chosen = "window" if len_hint >= 512 else "flat"
 
     diag = {"settle": {"launches": settle_n, "ms": round(settle_ms, 1)}}
     if scatter_diag is not None:

@@ -120,7 +120,6 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
                          uint32_t n, uint16_t *out, void *stream);
 
 /* Kernel selection for lvlip_csum_batch_dev_ex.  AUTO picks by len_hint:
- * >= 4096 B with n * len_hint >= 4 GiB -> WAVE (2 pieces, 8 waves/CU);
  * >= 512 B -> WINDOW (shape by the hint); otherwise or unknown ->
  * FLAT (measured: DESIGN.md §5). */
 #define LVLIP_KERNEL_AUTO        0  /* the default                                 */

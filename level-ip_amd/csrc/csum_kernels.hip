@@ -2188,10 +2188,10 @@ int window_group(int requested, int len_hint) {
     if (requested == 1 || requested == 2 || requested == 3 || requested == 4 || requested == 8)
         return requested;
     if (v == 1 || v == 2 || v == 3 || v == 4 || v == 8) return v;
-    if (len_hint <= 0) return 4;
-    if (len_hint >= 3072) return 1;
-    if (len_hint >= 1280) return 4;
-    return 8;
+    // no group in the request: as AUTO (dispatch_one) picks for this hint
+    if (len_hint >= 4096) return 3;
+    if (len_hint >= 2048) return 2;
+    return 4;
 }
 
 template <int R>
@@ -2281,19 +2281,15 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         // MTU/jumbo segments, the flat sweep on mixed header/payload batches and
         // stays within ~10 % elsewhere, so it is the choice when sizes are unknown.
         const int hint = cfg ? cfg->len_hint : 0;
-        if (hint >= 4096 && (uint64_t)n * (uint64_t)hint >= (4ull << 30)) {
-            // jumbo batches of >= 4 GiB: contiguous per-wave ranges stream
-            // 0.6 % faster than the interleaved deal (tcp9000)
-            kernel = LVLIP_KERNEL_WAVE;
-            if (wpc <= 0) wpc = 8;
-            if (unroll <= 0) unroll = 2;
-        } else if (hint >= 512) {
+        if (hint >= 512) {
             // the interleaved stream, shapes from scripts/shape_sweep.py
-            // (DESIGN.md §4): 2 pieces in flight per wave; groups of ~4-6 KB;
-            // more waves per CU for smaller packets (per-packet work)
+            // (DESIGN.md §4): 2 pieces in flight per wave; more waves per CU for
+            // smaller packets (per-packet work); groups of 4 packets up to 2 KiB,
+            // 2 up to 4 KiB, 3 for jumbo packets (power-of-two group bytes such as
+            // 2 x 4096 measured 3 % slow)
             kernel = LVLIP_KERNEL_WINDOW;
             if (wpc <= 0) wpc = hint < 1280 ? 16 : (hint < 2048 ? 12 : 8);
-            if (unroll <= 0) unroll = 2 | ((hint < 2048 ? 4 : (hint < 4096 ? 2 : 1)) << 8);
+            if (unroll <= 0) unroll = 2 | ((hint < 2048 ? 4 : (hint < 4096 ? 2 : 3)) << 8);
         } else {
             kernel = LVLIP_KERNEL_FLAT;
         }

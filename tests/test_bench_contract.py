@@ -54,7 +54,7 @@ COMMITTED = {
     "r02_bench_mixed.json": (1_639_948_630, 1.15),  # layout + descriptors, DESIGN.md §5
 }
 # the device function AUTO runs for each committed line (bench.py KERNEL_FN)
-DOMINANT = {"tcp1500": "k_window", "tcp9000": "k_stream", "mixed": "k_flat2"}
+DOMINANT = {"tcp1500": "k_window", "tcp9000": "k_window", "mixed": "k_flat2"}
 
 
 @pytest.mark.parametrize("name", sorted(COMMITTED))
