@@ -73,7 +73,8 @@ class Frame(ctypes.Structure):  # include/lvlip_skb.h: lvlip_frame
 
 
 # RX verdicts and flags (include/lvlip_skb.h)
-RX_OK, RX_NOT_IP, RX_SHORT, RX_BAD_VERSION, RX_BAD_IHL, RX_TTL0, RX_BAD_CSUM, RX_BAD_L4 = range(1, 9)
+RX_OK, RX_NOT_IP, RX_SHORT, RX_BAD_VERSION, RX_BAD_IHL, RX_TTL0, RX_BAD_CSUM, RX_BAD_L4, \
+    RX_UNKNOWN_PROTO = range(1, 10)
 RX_VERIFY_L4 = 0x1
 PLAN_MALFORMED = 0xFFFFFFFF
 

@@ -2,11 +2,14 @@
 run their checksums as one GPU batch; every frame is compared with the
 oracle's restatement of the reference's RX/TX decisions (oracle/skb_oracle.py)
 and, for config #1, with the reference stack's own echo replies."""
+import os
+
 import numpy as np
 import pytest
 
 import golden_io
 import lvlip
+import ref_rx_cases
 import skb_oracle
 import workloads
 from test_skb_cpu import _rx_cases, _scrambled_tcp_frames
@@ -203,3 +206,30 @@ def test_dev_frames_arguments():
     assert lib.lvlip_rx_verify_dev(p, f, 8, 0, o, None, s) == lvlip.OK  # headers filled above
     torch.cuda.synchronize()
     assert out.cpu().numpy().tolist() == [lvlip.RX_OK] * 8
+
+
+# ------------------------------------------- against level-ip's own ip_rcv --
+
+@pytest.mark.skipif(not os.path.exists(ref_rx_cases.REF_SO), reason="oracle/_ref/libref.so not built")
+def test_rx_verify_agrees_with_reference_ip_rcv(ctx):
+    """Batch-and-dispatch in front of level-ip's RX path: the
+    GPU batch accepts exactly the frames the reference's own ip_rcv accepts
+    (tests/ref_rx_child.py on oracle/_ref/libref.so: every drop reason, IP
+    options), host- and device-resident; and handing the stack only the frames
+    the batch accepted produces the same replies as handing it all of them."""
+    frs, kinds = ref_rx_cases.frames(8)
+    replies = ref_rx_cases.reference_replies(frs)
+    got = ctx.rx_verify(frs, 0)
+    assert [int(v) == lvlip.RX_OK for v in got] == [r is not None for r in replies]
+    got_l4 = ctx.rx_verify(frs, lvlip.RX_VERIFY_L4)
+    for v, k, r in zip(got_l4, kinds, replies):
+        if v == lvlip.RX_OK:
+            assert r is not None, k
+        if k == "icmp_csum":  # answered by the reference, caught by the L4 check
+            assert v == lvlip.RX_BAD_L4 and r is not None
+    buf, fd = lvlip.pack_frames(frs, align_mod=16, seed=3)
+    dev = lvlip.rx_verify_dev(_dev(buf), fd, 0).cpu().numpy()
+    assert np.array_equal(dev, got)
+    accepted = [f for f, v in zip(frs, got) if v == lvlip.RX_OK]
+    assert ref_rx_cases.reference_replies(accepted) == [r for r, v in zip(replies, got)
+                                                        if v == lvlip.RX_OK]
