@@ -478,6 +478,13 @@ def read_probe(lvlip, torch, base, stream):
                                                       nt, cus * bpc, stream.cuda_stream),
                    stream, reps=10)
         best[f"m{mode}u{u}nt{nt}b{bpc}"] = round(nb / ms / 1e6, 1)
+    # the chip-wide window order (4 KiB chunks dealt round robin, XCD-major,
+    # 8 waves/CU): the best plain read of the buffer measured
+    if cus % 4 == 0:
+        ms = timed(torch, lambda: lab.lvlip_lab_probe_chunk(base.data_ptr(), nb, sink.data_ptr(), 4, 4, 1,
+                                                            cus * 2, stream.cuda_stream),
+                   stream, reps=10)
+        best["window_c4"] = round(nb / ms / 1e6, 1)
     log("read_probe GB/s", best)
     return best
 

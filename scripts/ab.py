@@ -6,7 +6,8 @@
 A variant is kernel:unroll:waves_per_cu[:len_hint] (kernel names as bench.py's
 --kernel; len_hint defaults to the batch's average length).  A variant prefixed
 "alt/" runs through the library AB_ALT_LIB instead (another revision of the
-product, built by scripts/build_ab.sh), so two builds compare in one process.  After a clock
+product, built by scripts/build_ab.sh), so two builds compare in one process;
+"splitP/" runs the batch as P launches back to back on the stream.  After a clock
 settle, interleaved rounds in one process (AB_ROUNDS, default 5) each time every
 variant over 20 launches with HIP events; prints the median GB/s of algorithmic
 bytes per variant, and checks that every variant computes the same checksums.
@@ -58,6 +59,16 @@ def main():
         variants.append((v, f[0], int(f[1], 0), int(f[2]), int(f[3]) if len(f) > 3 else hint))
 
     def mk(k, u, w, h):
+        if k.startswith("split"):  # splitP/kernel: the batch as P launches back to back
+            parts, kk = int(k[5:k.index("/")]), k[k.index("/") + 1:]
+            cuts = [b.n * q // parts for q in range(parts + 1)]
+
+            def f():
+                for lo, hi in zip(cuts[:-1], cuts[1:]):
+                    lvlip.batch_dev(base.data_ptr(), descs.data_ptr() + 16 * lo, hi - lo,
+                                    out.data_ptr() + 2 * lo, s.cuda_stream, lvlip.KERNEL_NAMES[kk],
+                                    u, w, h)
+            return f
         if k.startswith("alt/"):
             cfg = lvlip.LaunchCfg(lvlip.KERNEL_NAMES[k[4:]], u, w, h)
 
