@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""k_stream launch shape vs packet length (diagnostic, GPU box): for uniform
-batches of L-byte packets (16-B aligned slots, ~1.5 GB), times every
-(pieces in flight R, waves per CU w) pair plus AUTO, interleaved rounds in one
-process.  The table behind AUTO's choice in dispatch_one (csum_kernels.hip).
+"""Launch shape vs packet length (diagnostic, GPU box): for uniform batches of
+L-byte packets (16-B aligned slots, ~1.5 GB), times AUTO, k_stream shapes
+(pieces in flight R x waves per CU w) and k_window shapes (R x w x group),
+interleaved rounds in one process.  The tables behind AUTO's choice in
+dispatch_one (csum_kernels.hip).
 
 env: SH_LENS (default 512,768,1024,1500,2048,3000,4096,9000),
      SH_SHAPES (default 2x8,2x16,3x8,3x12,4x8,4x16), SH_ROUNDS (2),
