@@ -123,12 +123,14 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
  * >= 512 B -> WINDOW (shape by the hint); otherwise or unknown ->
  * FLAT (measured: DESIGN.md §5). */
 #define LVLIP_KERNEL_AUTO        0  /* the default                                 */
-#define LVLIP_KERNEL_WAVE        1  /* one wavefront per packet, persistent stream */
+#define LVLIP_KERNEL_WAVE        1  /* one wavefront per packet, persistent stream,
+                                       contiguous ranges per wave (A/B)        */
 #define LVLIP_KERNEL_WAVE_LDS    2  /* one wave per packet, LDS-DMA staging (A/B)  */
 #define LVLIP_KERNEL_FLAT        3  /* chunk-balanced tile sweep (ragged batches)  */
 #define LVLIP_KERNEL_WAVE_SIMPLE 4  /* one wave per packet, one launch wave each   */
-#define LVLIP_KERNEL_WAVE_STATIC 6  /* WAVE with a static split only (A/B)        */
-#define LVLIP_KERNEL_WAVE_DYN    7  /* WAVE with a dynamic cross-XCD tail (A/B)   */
+#define LVLIP_KERNEL_WAVE_STATIC 6  /* retired round-1 A/B id: runs WAVE         */
+#define LVLIP_KERNEL_WAVE_DYN    7  /* retired round-1 A/B id (dynamic tail,
+                                       DESIGN.md §8): runs WAVE                */
 #define LVLIP_KERNEL_WINDOW      8  /* WAVE with packets dealt in small groups
                                        round robin over the grid (one narrow
                                        window of the batch in flight)          */

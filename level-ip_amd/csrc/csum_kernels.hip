@@ -38,10 +38,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <algorithm>
 #include <atomic>
-#include <mutex>
-#include <vector>
 
 #include "flat_src.h"
 #include "lvlip_csum.h"
@@ -199,15 +196,18 @@ __global__ __launch_bounds__(256) void k_wave_simple(const uint8_t* __restrict__
 }
 
 
-// ----------------------------------------------- k_stream (the default path) --
+// ---------------------------------- the ring (k_stream, k_window): building blocks --
 //
-// One wavefront per packet, persistent.  Wave w owns the contiguous packet
-// range [w*per_wave, (w+1)*per_wave) and streams through it with a ring of R
-// outstanding pieces; a piece is up to 2 KiB of one packet, read as two 1 KiB
-// wave-loads (64 lanes x 16 B, nontemporal).  The next packet's loads are
-// issued before the current packet is reduced.  The packet's last piece
-// triggers the DPP reduction and the fold; results gather in lane (p - g) of a
-// register and leave as one 128-B store per 64 packets.
+// One wavefront per packet, persistent.  Each wave streams through its packets
+// (which ones: the deal, below) with a ring of R outstanding pieces; a piece is
+// up to 2 KiB of one packet, read as two 1 KiB wave-loads (64 lanes x 16 B,
+// nontemporal).  The next packet's loads are issued before the current packet
+// is reduced.  The packet's last piece triggers the DPP reduction and the fold;
+// results gather in lane (k - gc) of a register and leave as one store per 64
+// packets.  A piece keeps all per-piece bookkeeping amortised over 2 KiB, so a
+// 1500-B segment is one piece (r01 profile of a per-1KiB-slot ring: ~130 SALU
+// per packet, the CU's scalar unit ~80 % busy and the kernel SALU-bound; this
+// layout cuts that ~3x).
 //
 // Addressing: a buffer resource per packet whose base is the packet's first
 // byte (any byte alignment; gfx950 buffer loads accept it) and whose
@@ -273,38 +273,6 @@ __device__ __forceinline__ uint32_t dot2_acc(uint32_t x, uint32_t acc) {
     return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, x), one, acc, false);
 }
 
-// Issued from asm so hipcc does not see an LDS-DMA in flight.
-__device__ __forceinline__ void fetch_window(const lvlip_csum_desc* __restrict__ descs,
-                                             uint32_t first, uint32_t n, uint32_t lane,
-                                             uint4* win /* LDS, 64 entries */) {
-    uint32_t i = first + lane;
-    i = i < n ? i : n - 1u;  // lanes past the batch re-read a valid descriptor
-    const lvlip_csum_desc* g = descs + i;
-    const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)win);
-    // m0 is reserved to the compiler, which warns on the clobber; nothing else in
-    // these kernels reads m0 (tests/test_isa.py checks every m0 write is ours).
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-    // s_nop 4: `lds` comes from v_readfirstlane (VALU->SGPR->use hazard) and an
-    // M0 write needs a wait state before an LDS-DMA reads it.
-    asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-                 :
-                 : "v"(g), "s"(lds)
-                 : "memory", "m0");
-#pragma clang diagnostic pop
-}
-
-__device__ __forceinline__ u32x4 window_desc(const uint4* win, uint32_t k) {
-    const uint4 d = win[k];  // uniform address: LDS broadcast
-    u32x4 r;
-    r.x = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.x);
-    r.y = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.y);
-    r.z = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.z);
-    r.w = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.w);
-    return r;
-}
-
 struct PacketMeta {
     u32x4 srd;        // buffer resource: base = first byte, num_records = round_up(len, 4)
     uint32_t tinfo;   // lc << 4 | tk << 2 | (len & 3): lc = chunk holding the last byte
@@ -335,385 +303,109 @@ __device__ __forceinline__ void piece_wait(u32x4& a, u32x4& b) {
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
 }
 
-// --------------------------------------- dynamic tail of k_stream (DYN = true) --
+// ------------------------------------------ the ring: k_stream and k_window --
 //
-// k_stream's static split leaves the kernel waiting on the slowest XCD: under a
-// full-chip stream the eight XCDs drain equal shares 5-9 % apart
-// (scripts/lab_timeline.py: waves of one XCD end within ~10 us of each other,
-// whole XCDs 20-30 us apart on 1.5 GB).  Here each streaming wave first sweeps
-// a static segment (most of its share), then takes further segments of `chunk`
-// packets claimed from eight pools, so fast XCDs take the work slow ones have
-// not reached:
+// One body, two deals of packets to the nw = 4 x grid waves:
 //
-//   pool q = packets [t0 + q*plen, min(t0 + (q+1)*plen, n)), head ctr[q*32]
-//   claim  = atomic add on a head; [old, old + k*chunk) ∩ pool, or "empty"
+//   k_stream (G = 0)  wave r owns the contiguous range [r p, r p + p), p = ceil(n/nw):
+//                     the nw waves in flight read nw streams spread over the batch;
+//   k_window (G > 0)  the packets are dealt in groups of G round robin over the
+//                     grid: wave r owns groups r, r + nw, r + 2 nw, ... (group j =
+//                     packets [jG, jG + G)), and its k-th packet is
 //
-// Who claims: a workgroup is 4 streaming waves + 1 claimer wave.  The claimer
-// does every global atomic and hands segments to its streamers through LDS
-// queues (one segment kept queued per streamer).  A streamer's vector-memory
-// counter therefore never holds an atomic: vmcnt retires in issue order, so a
-// contended atomic in a streamer's queue would stall its load ring behind it
-// (measured: a streamer-side claim version ran at 3.6 TB/s against 6.6 static).
+//                       gidx(k) = ((k / G) * nw + r) * G + k % G,
 //
-//   * the claimer starts on pool XCC_ID (speed only: correctness never depends
-//     on placement; every packet belongs to exactly one static segment or claim)
-//   * one atomic per claimer round covers every streamer that needs a segment
-//   * when its pool comes back short, the claimer reads all eight heads and
-//     moves to the pool with the most left; when none has any it posts "end"
-//     to its streamers (no claims on empty pools: see next_pool)
-//   * the last claimer to leave (exit counter ctr[9*32]) zeroes the heads and
-//     the counter, so the next launch on the same block starts clean
+//                     so the waves in flight read one narrow window of the batch
+//                     (nw x G packets) that slides through it.  Plain streaming
+//                     reads in that order run 3-6 % faster on MI355X than in nw
+//                     far-apart streams (scripts/lab_window.py).
 //
-// Windows: up to 64 packets of one segment; descriptors arrive by LDS-DMA into
-// the other half of the wave's double buffer while the current one is swept.
-// Results gather per window and leave as one store of up to 64 x 2 B.
-struct TailArgs {
-    uint32_t* ctr;    // counter block (zeroed before the first launch)
-    uint32_t t0;      // first pooled packet (= streaming waves * per_wave)
-    uint32_t plen;    // packets per pool
-    uint32_t chunk;   // packets per claim
-    uint32_t nblocks; // workgroups in the grid
-    unsigned long long* trace;  // diagnostics only (LVLIP_TAIL_TRACE): 8 u64 per streamer, or null
-    uint32_t epoch;   // FB: launch number on this counter block (host-counted, >= 1)
+// Everything else is local to the wave's packet sequence k = 0 .. cnt-1: the
+// descriptor windows hold the wave's packets 64k .. 64k+63 (the LDS-DMA takes a
+// per-lane address, so the interleaved gather costs nothing extra), and each
+// window's 64 results leave as one store with per-lane addresses (one 128-B
+// store for a contiguous range).
+//
+// k_window's ranks are XCD-major when the grid is a multiple of 8 blocks (block
+// b runs on XCD b % 8 as observed; placement is a speed matter only, every rank
+// is owned by exactly one wave whatever the placement): neighbouring groups then
+// belong to waves of one XCD, so the partial 32-B sectors of their 2-B results
+// merge in that XCD's L2 before they are written back.
+template <int G>
+struct Deal {
+    uint64_t nw, rank, p_lo;
+    uint32_t cnt;  // the wave's packets
+
+    // false when this wave has no packet
+    __device__ __forceinline__ bool init(uint32_t n, uint32_t wid) {
+        nw = (uint64_t)gridDim.x * SW_WAVES;
+        if (G == 0) {
+            rank = (uint64_t)blockIdx.x * SW_WAVES + wid;
+            const uint64_t per = ((uint64_t)n + nw - 1) / nw;
+            p_lo = rank * per;
+            if (p_lo >= n) return false;
+            cnt = (uint32_t)min<uint64_t>(per, (uint64_t)n - p_lo);
+            return true;
+        }
+        rank = (gridDim.x & 7u) == 0u
+                   ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * SW_WAVES + wid
+                   : (uint64_t)blockIdx.x * SW_WAVES + wid;
+        p_lo = 0;
+        // gcount groups, the last one short when it is the batch's last
+        const uint64_t ng = ((uint64_t)n + G - 1) / G;
+        if (rank >= ng) return false;
+        const uint64_t gcount = (ng - 1 - rank) / nw + 1;
+        const uint64_t glast = rank + (gcount - 1) * nw;
+        const uint64_t last_size = min<uint64_t>((uint64_t)(G > 0 ? G : 1), (uint64_t)n - glast * G);
+        cnt = (uint32_t)((gcount - 1) * G + last_size);
+        return true;
+    }
+    __device__ __forceinline__ uint64_t gidx(uint32_t k) const {
+        if (G == 0) return p_lo + k;
+        return ((uint64_t)(k / (G > 0 ? G : 1)) * nw + rank) * G + (k % (G > 0 ? G : 1));
+    }
 };
 
-// Counter words sit 8 KiB apart: atomics on one word serialise at the memory
-// channel that holds it, and words sharing a channel would stall that channel's
-// share of every wave's stream together (measured).
-constexpr uint32_t TAIL_STRIDE = 2048u;             // u32 words between counters
-constexpr uint32_t TAIL_GEXIT = 8u * TAIL_STRIDE;   // 8 exit counters (blockIdx % 8)
-constexpr uint32_t TAIL_FEXIT = 16u * TAIL_STRIDE;  // final exit counter
-constexpr uint32_t TAIL_WORDS = 17u * TAIL_STRIDE;
-constexpr uint32_t TQ = 4;  // queue slots per streamer (one is kept filled)
-
-// ------------------------------ slot weights from the last launch (FB = true) --
-//
-// Blocks are dealt round-robin over the XCDs and the mapping blockIdx % 8 ->
-// XCD is the same from launch to launch, and so is each XCD's streaming rate
-// (scripts/lab_placement.py: 12 launches, every block on XCD b % 8; per-slot
-// end times stable to a few us, 200-251 us apart at 16 waves/CU).  So an FB
-// launch gives slot s = blockIdx % 8 a share W_s of the batch, set from the
-// previous launch on the same counter block: W_s' ∝ W_s / duration_s (half way
-// there per launch, each within 3/4..5/4 of even), and every wave of the slot
-// an equal part of it.  The partition is a pure function of (n, grid, W), and
-// every wave reads the same W and durations (system-coherent loads of values
-// only the previous launch wrote), so the packets are covered exactly once
-// whatever the weights or placement; placement only decides whether it pays.
-// Per launch e: read W[(e-1)&1], D[(e-1)&1]; block 0 writes W[e&1]; each block
-// atomicMax-es (e << 32 | its longest wave duration) into D[e&1][slot].
-constexpr uint32_t FB_TOTAL = 1u << 24;             // weights' fixed-point sum
-static_assert(SW_WAVES == 4, "FB splits a slot's stripe share with >> 2");
-constexpr uint32_t FB_W = 64u;                      // W[2][8] u32 at words 64..79
-__device__ __forceinline__ uint32_t fb_d_word(uint32_t slot, uint32_t par) {
-    return (1u + slot) * TAIL_STRIDE + 16u + 2u * par;  // u64, 8 KiB apart per slot
+// Descriptors of the wave's packets [first, first + 64) into an LDS window by
+// LDS-DMA, one per lane; issued from asm so hipcc does not see it in flight.
+template <int G>
+__device__ __forceinline__ void fetch_window(const lvlip_csum_desc* __restrict__ descs,
+                                             const Deal<G>& dl, uint32_t first, uint32_t lane,
+                                             uint4* win /* LDS, 64 entries */) {
+    uint32_t k = first + lane;
+    k = k < dl.cnt ? k : dl.cnt - 1u;  // lanes past the wave's packets re-read a valid descriptor
+    const lvlip_csum_desc* g = descs + dl.gidx(k);
+    const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)win);
+    // m0 is reserved to the compiler, which warns on the clobber; nothing else in
+    // these kernels reads m0 (tests/test_isa.py checks every m0 write is ours).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    // s_nop 4: `lds` comes from v_readfirstlane (VALU->SGPR->use hazard) and an
+    // M0 write needs a wait state before an LDS-DMA reads it.
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :
+                 : "v"(g), "s"(lds)
+                 : "memory", "m0");
+#pragma clang diagnostic pop
 }
 
-// This launch's weights (identical in every wave).  Lanes 0-7 fetch W[s] and
-// D[s] of the previous launch in one round trip (two system-coherent vector
-// loads, one wait); the wave then reads them out lane by lane.
-__device__ __forceinline__ void fb_weights(const TailArgs& ta, uint32_t* w) {
-    const uint32_t pe = (ta.epoch - 1u) & 1u;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t l8 = lane & 7u;
-    const uint32_t* wa = ta.ctr + FB_W + pe * 8u + l8;
-    const uint32_t* da = ta.ctr + fb_d_word(l8, pe);
-    uint32_t wv;
-    uint64_t dv;
-    asm volatile(
-        "global_load_dword %0, %2, off sc0 sc1\n\t"
-        "global_load_dwordx2 %1, %3, off sc0 sc1\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(wv), "=&v"(dv)
-        : "v"(wa), "v"(da)
-        : "memory");
-    uint32_t wp[8];
-    uint64_t dur[8];
-    uint64_t wsum = 0;
-    bool ok = true;
-#pragma unroll
-    for (uint32_t s = 0; s < 8u; ++s) {
-        wp[s] = (uint32_t)__builtin_amdgcn_readlane((int)wv, (int)s);
-        const uint32_t dlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dv, (int)s);
-        const uint32_t dhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(dv >> 32), (int)s);
-        dur[s] = dlo;
-        ok = ok && dhi == ta.epoch - 1u && dlo != 0u;
-        wsum += wp[s];
-    }
-    ok = ok && wsum == FB_TOTAL;
-    constexpr uint32_t EVEN = FB_TOTAL / 8u;
-    if (!ok) {
-#pragma unroll
-        for (uint32_t s = 0; s < 8u; ++s) w[s] = EVEN;
-        return;
-    }
-    // IEEE double (exact for these magnitudes' products, correctly rounded
-    // quotients): every wave computes the same bits, and it avoids the
-    // software 64-bit integer divisions (~24 of them cost each wave ~8 us at
-    // start, measured)
-    double rate[8], rsum = 0.0;
-#pragma unroll
-    for (uint32_t s = 0; s < 8u; ++s) {
-        rate[s] = (double)wp[s] / (double)dur[s];
-        rsum += rate[s];
-    }
-    double v[8], vsum = 0.0;
-#pragma unroll
-    for (uint32_t s = 0; s < 8u; ++s) {
-        const double target = (double)FB_TOTAL * rate[s] / rsum;
-        double x = 0.5 * ((double)wp[s] + target);
-        x = x < 0.75 * EVEN ? 0.75 * EVEN : (x > 1.25 * EVEN ? 1.25 * EVEN : x);
-        v[s] = x;
-        vsum += x;
-    }
-    uint32_t acc = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < 7u; ++s) {
-        w[s] = (uint32_t)(v[s] * (double)FB_TOTAL / vsum);
-        acc += w[s];
-    }
-    w[7] = FB_TOTAL - acc;
-}
-
-__device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// The claimer wave of a DYN workgroup (see above); returns when every streamer
-// of its workgroup has been sent "end".
-__device__ __forceinline__ void tail_claimer(const TailArgs& ta, uint32_t n, uint32_t lane,
-                                             uint32_t (*q_lo)[TQ], uint32_t (*q_hi)[TQ],
-                                             uint32_t* q_tail, const uint32_t* q_head,
-                                             uint32_t* q_end) {
-    auto pool_lo = [&](uint32_t q) { return ta.t0 + q * ta.plen; };
-    auto pool_hi = [&](uint32_t q) {
-        return (uint32_t)min<uint64_t>((uint64_t)ta.t0 + (uint64_t)(q + 1u) * ta.plen, (uint64_t)n);
-    };
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    uint32_t q = xcc & 7u;          // current pool (uniform)
-    bool all_empty = false;         // every pool used up (uniform)
-    uint32_t pushed = 0;            // lane l < 4: segments pushed to streamer l
-    bool fin = lane >= SW_WAVES;    // lane l < 4: "end" posted to streamer l
-    // The current pool ran dry: read all eight heads (lanes 0-7, plain
-    // system-coherent loads) and move to the pool with the most left, or learn
-    // that none has any.  Atomics on one word serialise at its memory channel
-    // (~87 per us), and a claim on an empty pool is wasted; measured: claimers
-    // probing pools by claiming (and OR-ing an empty mask) slowed the whole
-    // chip's stream by up to 15 %.  Reads do not serialise.
-    auto next_pool = [&]() {
-        uint32_t head = 0xffffffffu;
-        if (lane < 8u) {
-            const uint32_t* hp = ta.ctr + lane * TAIL_STRIDE;
-            asm volatile("global_load_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
-                         : "=v"(head) : "v"(hp) : "memory");
-        }
-        const uint32_t pl = pool_lo(lane & 7u), ph = pool_hi(lane & 7u);
-        const uint32_t len = ph > pl ? ph - pl : 0u;
-        const uint32_t left = (lane < 8u && head < len) ? len - head : 0u;
-        uint32_t best = 0, bq = q;
-        for (uint32_t l = 0; l < 8u; ++l) {
-            const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)left, (int)l);
-            if (v > best) {
-                best = v;
-                bq = l;
-            }
-        }
-        all_empty = best == 0u;
-        q = bq;
-    };
-    if (pool_hi(q) <= pool_lo(q)) next_pool();  // an empty home pool (tiny tails)
-    for (;;) {
-        const bool need = !fin && pushed - lds_load(&q_head[lane & (SW_WAVES - 1)]) < 1u;
-        const uint64_t needm = __builtin_amdgcn_ballot_w64(need);
-        if (!needm) {
-            if (!__builtin_amdgcn_ballot_w64(!fin)) break;
-            // idle: sleep long (a polling claimer takes issue slots from its
-            // streamers); a streamer's pop wakes it (s_wakeup)
-            __builtin_amdgcn_s_sleep(127);
-            continue;
-        }
-        if (all_empty) {  // nothing left anywhere: post "end"
-            if (!fin) lds_store(&q_end[lane], 1u);
-            fin = true;
-            continue;
-        }
-        const uint32_t m = (uint32_t)__popcll(needm);
-        uint32_t old = 0;
-        if (lane == 0) old = atomicAdd(ta.ctr + q * TAIL_STRIDE, m * ta.chunk);
-        old = uniform(old);
-        const uint32_t pl = pool_lo(q), ph = pool_hi(q);
-        const uint32_t len = ph > pl ? ph - pl : 0u;
-        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(needm >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)needm, 0u));
-        const uint64_t st = (uint64_t)old + (uint64_t)r * ta.chunk;
-        if (need && st < len) {
-            const uint32_t slot = pushed % TQ;
-            lds_store(&q_lo[lane][slot], pl + (uint32_t)st);
-            lds_store(&q_hi[lane][slot], pl + (uint32_t)min<uint64_t>(st + ta.chunk, len));
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // segment before tail
-            lds_store(&q_tail[lane], pushed + 1u);
-            ++pushed;
-        }
-        if ((uint64_t)old + (uint64_t)m * ta.chunk >= len) next_pool();
-    }
-    // exit: the last claimer of each group (blockIdx % 8) counts the group out;
-    // the last group out zeroes every counter for the next launch
-    if (lane == 0) {
-        const uint32_t g = blockIdx.x & 7u;
-        const uint32_t in_g = (ta.nblocks - g + 7u) / 8u;
-        const uint32_t groups = ta.nblocks < 8u ? ta.nblocks : 8u;
-        if (atomicAdd(ta.ctr + TAIL_GEXIT + g * TAIL_STRIDE, 1u) == in_g - 1u &&
-            atomicAdd(ta.ctr + TAIL_FEXIT, 1u) == groups - 1u) {
-            for (uint32_t k = 0; k < 8u; ++k) {
-                atomicExch(ta.ctr + k * TAIL_STRIDE, 0u);
-                atomicExch(ta.ctr + TAIL_GEXIT + k * TAIL_STRIDE, 0u);
-            }
-            atomicExch(ta.ctr + TAIL_FEXIT, 0u);
-        }
-    }
-}
-
-// The ring is organised in pieces: a piece is up to 2 KiB of one packet (two
-// 1 KiB wave-loads, always both issued; chunks past the packet read zeros), so
-// all per-piece bookkeeping is amortised over 2 KiB and a 1500-B segment is one
-// piece.  R pieces are in flight; the oldest is retired by vmcnt(2*(R-1)).
-// (r01 profile of a per-1KiB-slot ring: ~130 SALU per packet, the CU's scalar
-// unit ~80 % busy and the kernel SALU-bound; this layout cuts that ~3x.)
-// DYN: the workgroup is 4 streamers + 1 claimer (tail_claimer above).  A
-// streamer's static segment is [wave*per_wave, ...) up to t0; when its current
-// segment enters its last window it pops the next segment from its LDS queue
-// (the pop's wait is one asm block: a loop in the C++ control flow here would
-// sit inside the ring loop and cost register copies on every packet) and
-// prefetches that segment's first window, so the ring runs on across segment
-// boundaries.  Everything a DYN launch changes sits on the window-entry path;
-// the per-packet path is the static kernel's plus one window-base word per
-// piece (results flush per window, and a window may end with its segment).
-template <int R, int POL = 0, bool DYN = false, bool FB = false>
-__global__ __launch_bounds__(DYN ? 320 : 256) void k_stream(const uint8_t* __restrict__ base,
-                                                const lvlip_csum_desc* __restrict__ descs,
-                                                uint32_t n, uint32_t per_wave, TailArgs ta,
-                                                uint16_t* __restrict__ out) {
-    __shared__ uint4 s_win[SW_WAVES][2][64];
-    // DYN: per streamer, a ring of segments [lo, hi), tail (claimer), head
-    // (streamer), end flag
-    __shared__ uint32_t q_lo[SW_WAVES][TQ], q_hi[SW_WAVES][TQ];
-    __shared__ uint32_t q_tail[SW_WAVES], q_head[SW_WAVES], q_end[SW_WAVES];
+template <int R, int G, int POL>
+__device__ __forceinline__ void ring_sweep(const uint8_t* __restrict__ base,
+                                           const lvlip_csum_desc* __restrict__ descs, uint32_t n,
+                                           uint16_t* __restrict__ out, uint4 (*s_win)[64]) {
     constexpr uint32_t END = 0xffffffffu;
     constexpr uint32_t PIECE = 2048u;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lane16 = lane * 16u;
     const uint32_t wid = uniform(threadIdx.x >> 6);
-    if (DYN) {
-        if (threadIdx.x < SW_WAVES) {
-            q_tail[threadIdx.x] = 0;
-            q_head[threadIdx.x] = 0;
-            q_end[threadIdx.x] = 0;
-        }
-        __syncthreads();
-        if (wid == SW_WAVES) {
-            tail_claimer(ta, n, lane, q_lo, q_hi, q_tail, q_head, q_end);
-            return;
-        }
-    }
-    const uint32_t wave = uniform(blockIdx.x * SW_WAVES + wid);
-    const unsigned long long t_start =
-        (FB || (DYN && ta.trace)) ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    __shared__ uint32_t fb_dmax, fb_cnt;
-    uint32_t p_lo, p_hi, fb_w_slot = 0;
-    if (FB) {
-        if (threadIdx.x == 0) {
-            fb_dmax = 0;
-            fb_cnt = 0;
-        }
-        uint32_t w[8];
-        fb_weights(ta, w);
-        const uint32_t slot = blockIdx.x & 7u;
-        fb_w_slot = w[slot];
-        if (blockIdx.x == 0 && wid == 0 && lane == 0) {  // next launch's input
-            uint32_t* wn = ta.ctr + FB_W + (ta.epoch & 1u) * 8u;
-#pragma unroll
-            for (uint32_t s = 0; s < 8u; ++s)
-                asm volatile("global_store_dword %0, %1, off sc0 sc1" :: "v"(wn + s), "v"(w[s]) : "memory");
-        }
-        // Stripes keep the static kernel's interleaving (every XCD reads the
-        // whole buffer; one contiguous region per XCD measured slower): stripe
-        // k = blockIdx / 8 covers [n*k/K, n*(k+1)/K), K = grid / 8, and slot s
-        // takes its W_s share of every stripe, split evenly over its 4 waves.
-        const uint32_t K = ta.nblocks >> 3;  // launcher: grid % 8 == 0
-        const uint32_t k = blockIdx.x >> 3;
-        // n*k < 2^45 is exact in double, and a quotient of integers below
-        // 2^53 that is not an integer lies at least 2^-45 (relative) from one,
-        // so the correctly rounded quotient floors to the integer quotient;
-        // every wave computes the same bits
-        const uint64_t S = (uint64_t)((double)n * (double)k / (double)K);
-        const uint64_t E = (uint64_t)((double)n * (double)(k + 1u) / (double)K);
-        const uint64_t L = E - S;
-        uint64_t c0 = 0;
-#pragma unroll
-        for (uint32_t s = 0; s < 8u; ++s) c0 += s < slot ? w[s] : 0u;
-        const uint64_t a0 = S + ((L * c0) >> 24);                 // FB_TOTAL = 2^24
-        const uint64_t b0 = S + ((L * (c0 + w[slot])) >> 24);
-        const uint64_t part = b0 - a0;
-        p_lo = (uint32_t)(a0 + ((part * wid) >> 2));                // SW_WAVES = 4
-        p_hi = (uint32_t)(a0 + ((part * (wid + 1u)) >> 2));
-        __syncthreads();  // fb_dmax / fb_cnt initialised before any wave's exit
-    } else {
-        const uint64_t lo64 = (uint64_t)wave * per_wave;
-        if (lo64 >= n) return;  // never with DYN (launcher: per_wave * waves <= n)
-        p_lo = (uint32_t)lo64;
-        p_hi = (uint32_t)min<uint64_t>(lo64 + per_wave, DYN ? (uint64_t)min(ta.t0, n) : (uint64_t)n);
-    }
+    Deal<G> dl;
+    if (!dl.init(n, wid)) return;
+    const uint32_t cnt = dl.cnt;
 
-    // DYN: the next segment, popped when the current one enters its last window
-    uint32_t n_lo = 0, n_hi = 0, popped = 0;
-    bool n_valid = false;
-    const uint32_t a_tail = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&q_tail[wid];
-    const uint32_t a_end = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&q_end[wid];
-    auto pop = [&]() {
-        uint32_t vt, ve, tail, fin;
-        asm volatile(
-            "1:\n\t"
-            "ds_read_b32 %0, %4\n\t"
-            "ds_read_b32 %1, %5\n\t"
-            "s_waitcnt lgkmcnt(0)\n\t"
-            "v_readfirstlane_b32 %2, %0\n\t"
-            "v_readfirstlane_b32 %3, %1\n\t"
-            "s_nop 1\n\t"
-            "s_cmp_gt_u32 %2, %6\n\t"
-            "s_cbranch_scc1 2f\n\t"
-            "s_cmp_lg_u32 %3, 0\n\t"
-            "s_cbranch_scc1 2f\n\t"
-            "s_wakeup\n\t"
-            "s_sleep 1\n\t"
-            "s_branch 1b\n"
-            "2:"
-            : "=&v"(vt), "=&v"(ve), "=&s"(tail), "=&s"(fin)
-            : "v"(a_tail), "v"(a_end), "s"(popped)
-            : "memory", "scc");
-        if (tail <= popped) {
-            // "end" was seen; the claimer writes tail before end, so a fresh
-            // read of tail is final
-            tail = uniform(lds_load(&q_tail[wid]));
-        }
-        n_valid = tail > popped;
-        if (n_valid) {
-            const uint32_t slot = popped % TQ;
-            n_lo = uniform(lds_load(&q_lo[wid][slot]));
-            n_hi = uniform(lds_load(&q_hi[wid][slot]));
-            ++popped;
-            lds_store(&q_head[wid], popped);
-            asm volatile("s_wakeup" ::: "memory");  // the claimer refills the queue
-        }
-    };
-
-    // descriptor windows: packets [p_lo + 64w, p_lo + 64w + 64) live in
-    // s_win[wid][w & 1] (DYN: the wn-th window of the wave in s_win[wid][wn & 1])
-    uint32_t wn = 0;
-    fetch_window(descs, p_lo, n, lane, s_win[wid][0]);
-    fetch_window(descs, p_lo + 64u, n, lane, s_win[wid][1]);
+    // descriptor windows: the wave's packets [64w, 64w + 64) live in s_win[w & 1]
+    fetch_window<G>(descs, dl, 0u, lane, s_win[0]);
+    fetch_window<G>(descs, dl, 64u, lane, s_win[1]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // Packet metadata for the issue cursor's window, one packet per lane (VALU,
@@ -722,284 +414,7 @@ __global__ __launch_bounds__(DYN ? 320 : 256) void k_stream(const uint8_t* __res
     // kernel SALU-bound: r01 profile.)
     uint32_t m_x, m_y, m_z, m_t, m_s;  // srd.x, srd.y, srd.z, tinfo, start of packet (window + lane)
     auto load_window_meta = [&](uint32_t w) {
-        const uint4 d = s_win[wid][w & 1u][lane];
-        const PacketMeta pm = packet_meta(base, u32x4{d.x, d.y, d.z, d.w});
-        m_x = pm.srd.x;
-        m_y = pm.srd.y;
-        m_z = pm.srd.z;
-        m_t = pm.tinfo;
-        m_s = pm.start;
-    };
-    load_window_meta(0);
-    // DYN, a static segment of one or two windows: the window after it is the
-    // next segment's first (per_wave >= 128 makes this a corner case)
-    if (DYN && p_lo + 64u >= p_hi) {
-        pop();
-        if (n_valid) {
-            fetch_window(descs, n_lo, n, lane, s_win[wid][1]);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-
-    // issue cursor: packet ip (k = ip - p_lo), byte offset io of the next piece in it
-    uint32_t ip = p_lo, io = 0;
-    u32x4 srd;
-    uint32_t tinfo, start;
-    auto pull = [&](uint32_t k) {  // k = packet index within its window
-        srd.x = (uint32_t)__builtin_amdgcn_readlane((int)m_x, (int)k);
-        srd.y = (uint32_t)__builtin_amdgcn_readlane((int)m_y, (int)k);
-        srd.z = (uint32_t)__builtin_amdgcn_readlane((int)m_z, (int)k);
-        srd.w = SRD_WORD3;
-        tinfo = (uint32_t)__builtin_amdgcn_readlane((int)m_t, (int)k);
-        start = (uint32_t)__builtin_amdgcn_readlane((int)m_s, (int)k);
-    };
-    pull(0);
-
-    // consume side: raw sums W and seeds of packets [gc, gc+64) gather in lanes
-    uint32_t gc = p_lo;
-    uint32_t res_w = 0, res_s = 0;
-    uint32_t acc = 0;
-
-    u32x4 va[R], vb[R];
-    // per piece: packet (END past the range), start_sum, and
-    // meta = last | (len & 3) << 1 | (byte offset of the last dword in the piece) << 3
-    // (DYN: that offset masked to 11 bits, bit 14 = the packet ends its segment;
-    // s_wb = first packet of the piece's window)
-    uint32_t s_pkt[R], s_start[R], s_meta[R], s_wb[R];
-
-    auto issue = [&](int r) {
-        const bool live = ip < p_hi;  // uniform
-        u32x4 sr = srd;
-        if (!live) sr.z = 0;  // past the range: every dword out of range -> zeros
-        const uint32_t off = lane16 + io;
-        va[r] = buffer_load_nt_asm<POL>(off, sr);
-        vb[r] = buffer_load_nt_asm<POL>(off + 1024u, sr);
-        // srd.z = round_up(len, 4): the piece is the packet's last when it reaches
-        // that (or the packet is empty)
-        const bool last = io + PIECE >= srd.z;
-        s_pkt[r] = live ? ip : END;
-        s_start[r] = start;
-        if (DYN) {
-            s_meta[r] = (uint32_t)last | ((tinfo & 3u) << 1) | ((((srd.z - 4u) - io) & 0x7FFu) << 3) |
-                        ((uint32_t)(last && ip + 1u == p_hi) << 14);
-            s_wb[r] = ip - ((ip - p_lo) & 63u);
-        } else {
-            s_meta[r] = (uint32_t)last | ((tinfo & 3u) << 1) | (((srd.z - 4u) - io) << 3);
-        }
-        if (live) {
-            if (!last) {
-                io += PIECE;
-            } else {
-                ++ip;
-                io = 0;
-                if (DYN && ip == p_hi && n_valid) {  // on to the next segment
-                    p_lo = n_lo;
-                    p_hi = n_hi;
-                    ip = p_lo;
-                    n_valid = false;
-                }
-                if (ip < p_hi) {
-                    const uint32_t k = ip - p_lo;
-                    if ((k & 63u) == 0u) {  // entered window k/64
-                        if (DYN) {
-                            // a short window's DMA may be only one piece old:
-                            // retire it (vector-memory ops retire in issue order)
-                            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                            ++wn;
-                            load_window_meta(wn);
-                            if (ip + 64u < p_hi) {
-                                fetch_window(descs, ip + 64u, n, lane, s_win[wid][(wn + 1u) & 1u]);
-                            } else {
-                                pop();
-                                if (n_valid) fetch_window(descs, n_lo, n, lane, s_win[wid][(wn + 1u) & 1u]);
-                            }
-                        } else {
-                            load_window_meta(k >> 6);
-                            fetch_window(descs, ip + 64u, n, lane, s_win[wid][((k >> 6) + 1u) & 1u]);
-                        }
-                    }
-                    pull(k & 63u);
-                }
-            }
-        }
-    };
-
-    auto consume = [&](int r) {
-        // Piece r's two loads are the oldest in flight: 2*(R-1) ring loads (and
-        // possibly result stores / window DMAs, which only make this stricter)
-        // were issued after them.
-        piece_wait<2 * (R - 1)>(va[r], vb[r]);
-        u32x4 x = va[r], y = vb[r];
-        const uint32_t meta = s_meta[r];
-        const uint32_t len3 = (meta >> 1) & 3u;
-        if ((meta & 1u) && len3) {  // uniform: keep bytes [0, len & 3) of the last dword
-            const uint32_t pos = DYN ? (meta >> 3) & 0x7FFu : meta >> 3;  // byte offset of that dword in the piece
-            const uint32_t m = (1u << (8u * len3)) - 1u;
-            const bool me = lane == ((pos >> 4) & 63u);
-            const uint32_t tk = (pos >> 2) & 3u;
-            const bool in_b = pos >= 1024u;
-            const uint32_t m0 = (me && tk == 0u) ? m : ~0u, m1 = (me && tk == 1u) ? m : ~0u;
-            const uint32_t m2 = (me && tk == 2u) ? m : ~0u, m3 = (me && tk == 3u) ? m : ~0u;
-            if (in_b) {
-                y.x &= m0; y.y &= m1; y.z &= m2; y.w &= m3;
-            } else {
-                x.x &= m0; x.y &= m1; x.z &= m2; x.w &= m3;
-            }
-        }
-        acc = dot2_acc(x.x, acc);
-        acc = dot2_acc(x.y, acc);
-        acc = dot2_acc(x.z, acc);
-        acc = dot2_acc(x.w, acc);
-        acc = dot2_acc(y.x, acc);
-        acc = dot2_acc(y.y, acc);
-        acc = dot2_acc(y.z, acc);
-        acc = dot2_acc(y.w, acc);
-        if (meta & 1u) {
-            const uint32_t w = wave_sum_dpp(acc);
-            acc = 0;
-            const uint32_t g0 = DYN ? s_wb[r] : gc;
-            const uint32_t k = s_pkt[r] - g0;
-            if (lane == k) {
-                res_w = w;
-                res_s = s_start[r];
-            }
-            if (k == 63u || (DYN ? (meta >> 14) & 1u : s_pkt[r] + 1u == p_hi)) {
-                // fold 64 results at once (src/utils.c:46-54, per lane)
-                uint32_t tt = res_s + res_w;
-                tt = (tt & 0xffffu) + (tt >> 16);
-                tt = (tt & 0xffffu) + (tt >> 16);
-                if (lane <= k) out[g0 + lane] = (uint16_t)~tt;
-                gc += 64u;
-            }
-        }
-    };
-
-#pragma unroll
-    for (int r = 0; r < R; ++r) issue(r);
-    bool done = false;
-    while (!done) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (s_pkt[r] == END) {
-                done = true;
-                break;
-            }
-            consume(r);
-            issue(r);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this wave left in flight
-    if (FB && lane == 0) {
-        // the block's longest wave, into D[e & 1][slot] for the next launch
-        const uint32_t d = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
-        __hip_atomic_fetch_max(&fb_dmax, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (__hip_atomic_fetch_add(&fb_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
-            SW_WAVES - 1u) {
-            const uint32_t dm = __hip_atomic_load(&fb_dmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            atomicMax(reinterpret_cast<unsigned long long*>(ta.ctr + fb_d_word(blockIdx.x & 7u, ta.epoch & 1u)),
-                      ((unsigned long long)ta.epoch << 32) | (dm ? dm : 1u));
-            if (ta.trace) {  // diagnostics: {duration, slot's weight, slot, epoch} per block
-                ta.trace[blockIdx.x * 2u] = ((unsigned long long)fb_w_slot << 32) | dm;
-                ta.trace[blockIdx.x * 2u + 1u] = ((unsigned long long)ta.epoch << 32) | (blockIdx.x & 7u);
-            }
-        }
-    }
-    if (DYN && ta.trace && lane == 0) {
-        uint32_t xid, hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xid));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        unsigned long long* t = ta.trace + (uint64_t)wave * 8u;
-        t[0] = t_start;
-        t[1] = 0;
-        t[2] = __builtin_amdgcn_s_memrealtime();
-        t[3] = popped;
-        t[4] = xid & 7u;
-        t[5] = per_wave;
-        t[6] = wid;
-        t[7] = hw;
-    }
-}
-
-// ------------------------------------- k_window (the interleaved stream path) --
-//
-// k_stream's ring, metadata and reduction, with a different deal of packets to
-// waves.  k_stream gives each wave one contiguous range, so the nw waves in
-// flight read nw streams spread over the whole batch.  Here the packets are
-// dealt in groups of G round robin over the grid: the wave of rank r owns
-// groups r, r + nw, r + 2 nw, ... (group j = packets [jG, jG + G)), and its
-// k-th packet is
-//
-//   gidx(k) = ((k / G) * nw + r) * G + k % G.
-//
-// The waves in flight then read one narrow window of the batch (nw x G packets,
-// ~6-9 MB for MTU packets) that slides through it.  Plain streaming reads in that
-// order run 3-6 % faster on MI355X than in nw far-apart streams
-// (scripts/lab_window.py).
-//
-// Everything else is local to the wave's packet sequence k = 0 .. cnt-1: the
-// descriptor windows hold the wave's packets 64k .. 64k+63 (the LDS-DMA takes a
-// per-lane address, so the gather costs nothing extra), and each window's 64
-// results leave as one store with per-lane addresses.
-//
-// Ranks are XCD-major when the grid is a multiple of 8 blocks (block b runs on
-// XCD b % 8 as observed; placement is a speed matter only, every rank is owned
-// by exactly one wave whatever the placement): neighbouring groups then belong
-// to waves of one XCD, so the partial 32-B sectors of their 2-B results merge in
-// that XCD's L2 before they are written back.
-template <int G>
-__device__ __forceinline__ uint64_t window_gidx(uint32_t k, uint64_t nw, uint64_t rank) {
-    return ((uint64_t)(k / G) * nw + rank) * G + (k % G);
-}
-
-template <int G>
-__device__ __forceinline__ void fetch_window_il(const lvlip_csum_desc* __restrict__ descs,
-                                                uint32_t first, uint32_t cnt, uint64_t nw,
-                                                uint64_t rank, uint32_t lane,
-                                                uint4* win /* LDS, 64 entries */) {
-    uint32_t k = first + lane;
-    k = k < cnt ? k : cnt - 1u;  // lanes past the wave's packets re-read a valid descriptor
-    const lvlip_csum_desc* g = descs + window_gidx<G>(k, nw, rank);
-    const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)win);
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-    asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-                 :
-                 : "v"(g), "s"(lds)
-                 : "memory", "m0");
-#pragma clang diagnostic pop
-}
-
-template <int R, int G>
-__global__ __launch_bounds__(256) void k_window(const uint8_t* __restrict__ base,
-                                                const lvlip_csum_desc* __restrict__ descs,
-                                                uint32_t n, uint16_t* __restrict__ out) {
-    __shared__ uint4 s_win[SW_WAVES][2][64];
-    constexpr uint32_t END = 0xffffffffu;
-    constexpr uint32_t PIECE = 2048u;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lane16 = lane * 16u;
-    const uint32_t wid = uniform(threadIdx.x >> 6);
-    const uint64_t nw = (uint64_t)gridDim.x * SW_WAVES;
-    const uint64_t rank =
-        (gridDim.x & 7u) == 0u
-            ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * SW_WAVES + wid
-            : (uint64_t)blockIdx.x * SW_WAVES + wid;
-    // this wave's packets: gcount groups, the last one short when it is the batch's last
-    const uint64_t ng = ((uint64_t)n + G - 1) / G;
-    if (rank >= ng) return;
-    const uint64_t gcount = (ng - 1 - rank) / nw + 1;
-    const uint64_t glast = rank + (gcount - 1) * nw;
-    const uint64_t last_size = min<uint64_t>((uint64_t)G, (uint64_t)n - glast * G);
-    const uint32_t cnt = (uint32_t)((gcount - 1) * G + last_size);
-
-    fetch_window_il<G>(descs, 0u, cnt, nw, rank, lane, s_win[wid][0]);
-    fetch_window_il<G>(descs, 64u, cnt, nw, rank, lane, s_win[wid][1]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-    uint32_t m_x, m_y, m_z, m_t, m_s;  // metadata of packet (window + lane), as k_stream
-    auto load_window_meta = [&](uint32_t w) {
-        const uint4 d = s_win[wid][w & 1u][lane];
+        const uint4 d = s_win[w & 1u][lane];
         const PacketMeta pm = packet_meta(base, u32x4{d.x, d.y, d.z, d.w});
         m_x = pm.srd.x;
         m_y = pm.srd.y;
@@ -1012,7 +427,7 @@ __global__ __launch_bounds__(256) void k_window(const uint8_t* __restrict__ base
     uint32_t ip = 0, io = 0;  // issue cursor: the wave's packet ip, byte offset io in it
     u32x4 srd;
     uint32_t tinfo, start;
-    auto pull = [&](uint32_t k) {
+    auto pull = [&](uint32_t k) {  // k = packet index within its window
         srd.x = (uint32_t)__builtin_amdgcn_readlane((int)m_x, (int)k);
         srd.y = (uint32_t)__builtin_amdgcn_readlane((int)m_y, (int)k);
         srd.z = (uint32_t)__builtin_amdgcn_readlane((int)m_z, (int)k);
@@ -1033,10 +448,12 @@ __global__ __launch_bounds__(256) void k_window(const uint8_t* __restrict__ base
     auto issue = [&](int r) {
         const bool live = ip < cnt;  // uniform
         u32x4 sr = srd;
-        if (!live) sr.z = 0;
+        if (!live) sr.z = 0;  // past the range: every dword out of range -> zeros
         const uint32_t off = lane16 + io;
-        va[r] = buffer_load_nt_asm<0>(off, sr);
-        vb[r] = buffer_load_nt_asm<0>(off + 1024u, sr);
+        va[r] = buffer_load_nt_asm<POL>(off, sr);
+        vb[r] = buffer_load_nt_asm<POL>(off + 1024u, sr);
+        // srd.z = round_up(len, 4): the piece is the packet's last when it reaches
+        // that (or the packet is empty)
         const bool last = io + PIECE >= srd.z;
         s_pkt[r] = live ? ip : END;
         s_start[r] = start;
@@ -1050,8 +467,7 @@ __global__ __launch_bounds__(256) void k_window(const uint8_t* __restrict__ base
                 if (ip < cnt) {
                     if ((ip & 63u) == 0u) {  // entered window ip/64
                         load_window_meta(ip >> 6);
-                        fetch_window_il<G>(descs, ip + 64u, cnt, nw, rank, lane,
-                                           s_win[wid][((ip >> 6) + 1u) & 1u]);
+                        fetch_window<G>(descs, dl, ip + 64u, lane, s_win[((ip >> 6) + 1u) & 1u]);
                     }
                     pull(ip & 63u);
                 }
@@ -1060,12 +476,15 @@ __global__ __launch_bounds__(256) void k_window(const uint8_t* __restrict__ base
     };
 
     auto consume = [&](int r) {
+        // Piece r's two loads are the oldest in flight: 2*(R-1) ring loads (and
+        // possibly result stores / window DMAs, which only make this stricter)
+        // were issued after them.
         piece_wait<2 * (R - 1)>(va[r], vb[r]);
         u32x4 x = va[r], y = vb[r];
         const uint32_t meta = s_meta[r];
         const uint32_t len3 = (meta >> 1) & 3u;
         if ((meta & 1u) && len3) {  // uniform: keep bytes [0, len & 3) of the last dword
-            const uint32_t pos = meta >> 3;
+            const uint32_t pos = meta >> 3;  // byte offset of that dword in the piece
             const uint32_t m = (1u << (8u * len3)) - 1u;
             const bool me = lane == ((pos >> 4) & 63u);
             const uint32_t tk = (pos >> 2) & 3u;
@@ -1095,10 +514,11 @@ __global__ __launch_bounds__(256) void k_window(const uint8_t* __restrict__ base
                 res_s = s_start[r];
             }
             if (k == 63u || s_pkt[r] + 1u == cnt) {
-                uint32_t tt = res_s + res_w;  // src/utils.c:46-54, per lane
+                // fold 64 results at once (src/utils.c:46-54, per lane)
+                uint32_t tt = res_s + res_w;
                 tt = (tt & 0xffffu) + (tt >> 16);
                 tt = (tt & 0xffffu) + (tt >> 16);
-                if (lane <= k) out[window_gidx<G>(gc + lane, nw, rank)] = (uint16_t)~tt;
+                if (lane <= k) out[dl.gidx(gc + lane)] = (uint16_t)~tt;
                 gc += 64u;
             }
         }
@@ -1118,7 +538,25 @@ __global__ __launch_bounds__(256) void k_window(const uint8_t* __restrict__ base
             issue(r);
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this wave left in flight
+}
+
+// POL: the data loads' cache policy (A/B, LVLIP_LOAD_POLICY)
+template <int R, int POL = 0>
+__global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base,
+                                                const lvlip_csum_desc* __restrict__ descs,
+                                                uint32_t n, uint16_t* __restrict__ out) {
+    __shared__ uint4 s_win[SW_WAVES][2][64];
+    ring_sweep<R, 0, POL>(base, descs, n, out, s_win[uniform(threadIdx.x >> 6)]);
+}
+
+template <int R, int G>
+__global__ __launch_bounds__(256) void k_window(const uint8_t* __restrict__ base,
+                                                const lvlip_csum_desc* __restrict__ descs,
+                                                uint32_t n, uint16_t* __restrict__ out) {
+    static_assert(G > 0, "k_window deals groups of G >= 1 packets");
+    __shared__ uint4 s_win[SW_WAVES][2][64];
+    ring_sweep<R, G, 0>(base, descs, n, out, s_win[uniform(threadIdx.x >> 6)]);
 }
 
 // ------------------------------------------------- k_wave_lds (LDS-DMA path) --
@@ -1961,30 +1399,23 @@ size_t flat_lds_pad() {
     return v;
 }
 
-template <int U>
-bool launch_stream_fb(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
-                      uint32_t n, uint32_t per_wave, uint16_t* out);
-
-// fb: weight the eight blockIdx % 8 slots by the last launch's timing (FB, see
-// fb_weights; LVLIP_STREAM_FB=1); falls back to the plain static split when it
-// does not apply.
+// k_stream: waves_per_cu waves on every CU (fewer when the batch has fewer
+// packets), whole 256-thread blocks; each wave owns a contiguous range of
+// ceil(n / waves) packets.
 template <int U>
 void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
-                   uint32_t n, uint16_t* out, bool fb = false) {
+                   uint32_t n, uint16_t* out) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     uint64_t waves = (uint64_t)cu_count(dev) * (uint64_t)waves_per_cu;
     if (waves > n) waves = n;
     waves = (waves + 3) & ~3ull;  // whole 256-thread blocks
-    const uint32_t per_wave = (uint32_t)(((uint64_t)n + waves - 1) / waves);
     const uint32_t grid = (uint32_t)(waves / 4);
-    lvlip::TailArgs ta{};  // static split: no counter block
-    if (fb && launch_stream_fb<U>(grid, s, base, d, n, per_wave, out)) return;
     switch (load_policy()) {
 #define LVLIP_STREAM_POL(P)                                                              \
     case P:                                                                              \
         hipLaunchKernelGGL((lvlip::k_stream<U, P>), dim3(grid), dim3(256), 0, s,         \
-                           (const uint8_t*)base, d, n, per_wave, ta, out);               \
+                           (const uint8_t*)base, d, n, out);                             \
         break;
         LVLIP_STREAM_POL(1)
         LVLIP_STREAM_POL(2)
@@ -1993,172 +1424,8 @@ void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvli
 #undef LVLIP_STREAM_POL
         default:
             hipLaunchKernelGGL((lvlip::k_stream<U, 0>), dim3(grid), dim3(256), 0, s,
-                               (const uint8_t*)base, d, n, per_wave, ta, out);
+                               (const uint8_t*)base, d, n, out);
     }
-}
-
-// ---- dynamic tail of the stream kernel (k_stream<.., DYN = true>) ----
-//
-// Counter blocks: one per (device, stream), from a per-device pool allocated
-// and zeroed once.  Launches on one stream are serialised, so they may share a
-// block (each launch's last wave zeroes it for the next).  A launch captured
-// into a HIP graph gets a block of its own that nothing else uses (a graph
-// holding a batch must not be replayed concurrently with itself, as with any
-// kernel that owns scratch).  When no block is available (pool exhausted, the
-// per-thread default stream, first use while capturing) the launch uses the
-// static split.
-constexpr int kTailSlots = 64;  // 139 KiB each
-
-struct TailPool {
-    uint32_t* mem = nullptr;
-    bool failed = false;
-    int used = 0;
-    std::vector<std::pair<uintptr_t, int>> by_stream;
-    uint32_t epoch[kTailSlots] = {};  // FB launches so far, per block
-};
-std::mutex g_tail_mu;
-TailPool g_tail[64];
-
-// epoch (optional): incremented for the block and returned (FB launches).
-uint32_t* tail_block(int dev, hipStream_t s, uint32_t* epoch = nullptr) {
-    if (dev < 0 || dev >= 64 || s == hipStreamPerThread) return nullptr;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess) return nullptr;
-    const bool capturing = cs != hipStreamCaptureStatusNone;
-    std::lock_guard<std::mutex> lk(g_tail_mu);
-    TailPool& p = g_tail[dev];
-    if (!p.mem) {
-        if (p.failed || capturing) return nullptr;
-        const size_t bytes = (size_t)kTailSlots * lvlip::TAIL_WORDS * 4u;
-        void* m = nullptr;
-        if (hipMalloc(&m, bytes) != hipSuccess || hipMemset(m, 0, bytes) != hipSuccess ||
-            hipDeviceSynchronize() != hipSuccess) {
-            if (m) (void)hipFree(m);
-            p.failed = true;
-            (void)hipGetLastError();
-            return nullptr;
-        }
-        p.mem = (uint32_t*)m;
-    }
-    int slot = -1;
-    if (!capturing)
-        for (const auto& e : p.by_stream)
-            if (e.first == (uintptr_t)s) slot = e.second;
-    if (slot < 0) {
-        if (p.used >= kTailSlots) return nullptr;
-        slot = p.used++;
-        if (!capturing) p.by_stream.emplace_back((uintptr_t)s, slot);
-    }
-    if (epoch) {
-        if (++p.epoch[slot] == 0) p.epoch[slot] = 1;  // 0 is "never launched"
-        *epoch = p.epoch[slot];
-    }
-    return p.mem + (size_t)slot * lvlip::TAIL_WORDS;
-}
-
-// LVLIP_STREAM_FB=1 turns the slot weights on (A/B, off by default: k_stream's
-// slots already end within ~3 % of each other); read once.
-bool fb_enabled() {
-    static const bool v = [] {
-        const char* e = getenv("LVLIP_STREAM_FB");
-        return e && strcmp(e, "1") == 0;
-    }();
-    return v;
-}
-
-template <int U>
-bool launch_stream_fb(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
-                      uint32_t n, uint32_t per_wave, uint16_t* out) {
-    // every slot needs blocks, and enough packets per wave to be worth it
-    if (grid < 8u || (grid & 7u) || per_wave < 64u || load_policy() != 0) return false;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    lvlip::TailArgs ta{};
-    ta.ctr = tail_block(dev, s, &ta.epoch);
-    if (!ta.ctr) return false;
-    static const bool freeze = getenv("LVLIP_FB_FREEZE") != nullptr;  // diagnostic: even weights
-    if (freeze) ta.epoch = 1;
-    static unsigned long long* const trace = [] {
-        const char* e = getenv("LVLIP_FB_TRACE");  // device address (diagnostics)
-        return e ? (unsigned long long*)(uintptr_t)strtoull(e, nullptr, 0) : nullptr;
-    }();
-    ta.trace = trace;
-    ta.nblocks = grid;
-    hipLaunchKernelGGL((lvlip::k_stream<U, 0, false, true>), dim3(grid), dim3(256), 0, s,
-                       (const uint8_t*)base, d, n, per_wave, ta, out);
-    return true;
-}
-
-// LVLIP_TAIL_PCT: share of the batch left to claims (default 0 = static split,
-// k_stream; the dynamic tail is an A/B variant until it measures faster:
-// DESIGN.md §8); LVLIP_TAIL_CHUNK: bytes per claim (default 16384).  Read once.
-int tail_pct() {
-    static const int v = [] {
-        const char* e = getenv("LVLIP_TAIL_PCT");
-        const int x = e ? atoi(e) : 0;
-        return x < 0 ? 0 : (x > 90 ? 90 : x);
-    }();
-    return v;
-}
-int tail_chunk_bytes() {
-    static const int v = [] {
-        const char* e = getenv("LVLIP_TAIL_CHUNK");
-        const int x = e ? atoi(e) : 16384;
-        return x < 1024 ? 1024 : x;
-    }();
-    return v;
-}
-
-// Returns false when the dynamic tail does not apply (caller falls back to
-// the static launch).
-template <int U>
-bool launch_stream_dyn(int waves_per_cu, hipStream_t s, const void* base,
-                       const lvlip_csum_desc* d, uint32_t n, uint16_t* out, int len_hint,
-                       bool explicit_dyn) {
-    // WAVE_DYN uses LVLIP_TAIL_PCT or 15; WAVE only when LVLIP_TAIL_PCT > 0
-    const int pct = explicit_dyn && getenv("LVLIP_TAIL_PCT") == nullptr ? 15 : tail_pct();
-    // diagnostic: LVLIP_TAIL_FORCE runs this kernel with pct 0 (static shares
-    // covering the batch, empty pools) to price the kernel's own structure
-    static const bool force = getenv("LVLIP_TAIL_FORCE") != nullptr;
-    if (pct == 0 && !force) return false;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const uint64_t waves = ((uint64_t)cu_count(dev) * (uint64_t)waves_per_cu + 3) & ~3ull;
-    // each streaming wave's static segment must span two windows (its first
-    // two descriptor windows are filled before it ever asks for a claim)
-    const uint64_t per_wave = pct == 0 ? ((uint64_t)n + waves - 1) / waves
-                                       : (uint64_t)n * (uint64_t)(100 - pct) / 100u / waves;
-    if (per_wave < 128) return false;
-    uint32_t* ctr = tail_block(dev, s);
-    if (!ctr) return false;
-    const uint64_t t0 = std::min<uint64_t>(per_wave * waves, n);
-    const int hint = len_hint > 0 ? len_hint : 1500;
-    lvlip::TailArgs ta;
-    ta.ctr = ctr;
-    ta.t0 = (uint32_t)t0;
-    ta.plen = (uint32_t)(((uint64_t)n - t0 + 7u) / 8u);
-    ta.chunk = (uint32_t)std::max(1, tail_chunk_bytes() / hint);
-    ta.nblocks = (uint32_t)(waves / 4);
-    static unsigned long long* const trace = [] {
-        const char* e = getenv("LVLIP_TAIL_TRACE");  // device address (diagnostics)
-        return e ? (unsigned long long*)(uintptr_t)strtoull(e, nullptr, 0) : nullptr;
-    }();
-    ta.trace = trace;
-    const uint32_t grid = (uint32_t)(waves / 4);
-    const uint32_t pw = (uint32_t)per_wave;
-    switch (load_policy()) {
-#define LVLIP_DYN_POL(P)                                                                 \
-    case P:                                                                              \
-        hipLaunchKernelGGL((lvlip::k_stream<U, P, true>), dim3(grid), dim3(320), 0, s,   \
-                           (const uint8_t*)base, d, n, pw, ta, out);                     \
-        break;
-        LVLIP_DYN_POL(1)
-#undef LVLIP_DYN_POL
-        default:
-            hipLaunchKernelGGL((lvlip::k_stream<U, 0, true>), dim3(grid), dim3(320), 0, s,
-                               (const uint8_t*)base, d, n, pw, ta, out);
-    }
-    return true;
 }
 
 // k_window: waves_per_cu waves on every CU (fewer when the batch has fewer
@@ -2299,29 +1566,16 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         case LVLIP_KERNEL_WAVE:
         case LVLIP_KERNEL_WAVE_STATIC:
         case LVLIP_KERNEL_WAVE_DYN: {
-            // unroll = 2-KiB pieces in flight per wave (2 = up to 4 KiB).
-            // WAVE_STATIC: static split (k_stream); WAVE_DYN: dynamic tail
-            // (k_stream<.., DYN>) where it applies; WAVE: static unless
-            // LVLIP_TAIL_PCT > 0 (DESIGN.md §8 has the measurements).
+            // k_stream: contiguous ranges (A/B against the window deal); unroll =
+            // 2-KiB pieces in flight per wave.  WAVE_STATIC and WAVE_DYN are the
+            // ids of round 1's split and dynamic-tail variants;
+            // both run the contiguous split now.
             if (unroll <= 0) unroll = 2;
             const int w = wpc > 0 ? wpc : 16;
-            const bool dyn = kernel != LVLIP_KERNEL_WAVE_STATIC;
-            const bool xd = kernel == LVLIP_KERNEL_WAVE_DYN;
-            const int hint = cfg ? cfg->len_hint : 0;
-            const bool fb = kernel == LVLIP_KERNEL_WAVE && fb_enabled();
             switch (unroll) {
-                case 2:
-                    if (!dyn || !launch_stream_dyn<2>(w, s, base, descs, n, out, hint, xd))
-                        launch_stream<2>(w, s, base, descs, n, out, fb);
-                    break;
-                case 3:
-                    if (!dyn || !launch_stream_dyn<3>(w, s, base, descs, n, out, hint, xd))
-                        launch_stream<3>(w, s, base, descs, n, out, fb);
-                    break;
-                case 4:
-                    if (!dyn || !launch_stream_dyn<4>(w, s, base, descs, n, out, hint, xd))
-                        launch_stream<4>(w, s, base, descs, n, out, fb);
-                    break;
+                case 2: launch_stream<2>(w, s, base, descs, n, out); break;
+                case 3: launch_stream<3>(w, s, base, descs, n, out); break;
+                case 4: launch_stream<4>(w, s, base, descs, n, out); break;
                 default: return LVLIP_EINVAL;
             }
             break;

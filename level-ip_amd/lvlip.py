@@ -29,11 +29,10 @@ LAB_PATH = os.path.join(HERE, "liblvlip_lab.so")
 # error codes (include/lvlip_csum.h)
 OK, EINVAL, ENODEV, EHIP, ENOMEM, ERANGE = 0, -1, -2, -3, -4, -5
 KERNEL_AUTO, KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_FLAT, KERNEL_WAVE_SIMPLE = 0, 1, 2, 3, 4
-KERNEL_WAVE_STATIC, KERNEL_WAVE_DYN, KERNEL_WINDOW, KERNEL_WFLAT = 6, 7, 8, 9
+KERNEL_WINDOW, KERNEL_WFLAT = 8, 9  # (6, 7: retired round-1 A/B ids, run WAVE)
 REG_DMA, REG_ZEROCOPY = 0, 1
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "wave_lds": KERNEL_WAVE_LDS,
                 "flat": KERNEL_FLAT, "wave_simple": KERNEL_WAVE_SIMPLE, "flat_v1": 5,
-                "wave_static": KERNEL_WAVE_STATIC, "wave_dyn": KERNEL_WAVE_DYN,
                 "window": KERNEL_WINDOW, "wflat": KERNEL_WFLAT}
 
 # struct lvlip_csum_desc {u64 offset; i32 len; u32 start_sum;}  (16 B)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Runs chosen kernels on one resident workload (for rocprofv3 passes):
-  RK_WORKLOAD=tcp1500 RK_KERNELS=wave,wave_static RK_REPS=10 python3 scripts/run_kernels.py"""
+  RK_WORKLOAD=tcp1500 RK_KERNELS=window,wave RK_REPS=10 python3 scripts/run_kernels.py"""
 import os
 import sys
 
@@ -15,7 +15,7 @@ b = workloads.make(os.environ.get("RK_WORKLOAD", "tcp1500"))
 base, descs, out = workloads.to_device(b)
 hint = b.algo_bytes // b.n
 for _ in range(int(os.environ.get("RK_REPS", "10"))):
-    for k in os.environ.get("RK_KERNELS", "wave,wave_static").split(","):
+    for k in os.environ.get("RK_KERNELS", "window,wave").split(","):
         lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_NAMES[k], len_hint=hint)
 torch.cuda.synchronize()
 print("ok")

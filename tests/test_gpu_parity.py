@@ -29,8 +29,6 @@ VARIANTS = [
     (lvlip.KERNEL_WAVE, 4, 0),
     (lvlip.KERNEL_WAVE, 2, 1),     # 1 wave/CU: long per-wave ranges, window refills
     (lvlip.KERNEL_WAVE, 4, 24),
-    (lvlip.KERNEL_WAVE_STATIC, 2, 0),  # stream kernel, static split only (A/B)
-    (lvlip.KERNEL_WAVE_DYN, 2, 1),     # dynamic tail where it applies (A/B)
     (lvlip.KERNEL_WAVE_SIMPLE, 1, 0),
     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0),
     (lvlip.KERNEL_WAVE_SIMPLE, 4, 8),
@@ -221,7 +219,6 @@ def test_full_size_bit_exact(name):
     for variant in [(lvlip.KERNEL_WAVE, 4, 0), (lvlip.KERNEL_WAVE, 3, 4),
                     (lvlip.KERNEL_WINDOW, 3, 0), (lvlip.KERNEL_WINDOW, 2, 0),
                     (lvlip.KERNEL_WFLAT, 0, 0), (lvlip.KERNEL_WFLAT, 8 | (64 << 8), 16),
-                    (lvlip.KERNEL_WAVE_DYN, 2, 0), (lvlip.KERNEL_WAVE_DYN, 2, 8),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
                     (lvlip.KERNEL_AUTO, 0, 0)]:
@@ -462,78 +459,26 @@ def test_batch_dev_on_user_stream_and_graph():
     assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
 
 
-@pytest.mark.parametrize("name,n,hint", [("tcp1500", 60000, 1500), ("tcp1500", 60000, 16384),
-                                         ("tcp9000", 40000, 9000), ("mixed", 40000, 200),
-                                         ("mixed", 40000, 0)])
-def test_stream_dynamic_tail(name, n, hint):
-    """k_stream_dyn (the stream kernel's dynamic tail): with 1 wave per CU the
-    static segments are >= 128 packets, so claims run even at these sizes; the
-    hint sets the claim size (1500 -> 10 packets, 16384 -> 1, 200 -> 81, 0 ->
-    10).  Back-to-back launches on one stream reuse one counter block (the last
-    wave resets it), two streams run concurrently with blocks of their own, and
-    a graph replay uses a block of its own: every run must be bit-exact."""
-    b = workloads.make(name, n=n)
-    base, descs, out = workloads.to_device(b)
-    want = pyoracle.batch(base.cpu().numpy(), b.descs, threads=THREADS)
-    for wpc, unroll in [(1, 2), (1, 3), (1, 4)]:
-        for rep in range(4):
-            out.fill_(0)
-            lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_WAVE_DYN, unroll=unroll,
-                              waves_per_cu=wpc, len_hint=hint)
-            torch.cuda.synchronize()
-            got = out.cpu().numpy().view(np.uint16)
-            bad = np.nonzero(got != want)[0]
-            assert bad.size == 0, (wpc, unroll, rep, bad.size, bad[:5])
-    # two streams at once, each with its own counter block, several launches deep
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    outs = [torch.zeros_like(out) for _ in range(6)]
-    for i, o in enumerate(outs):
-        s = s1 if i % 2 == 0 else s2
-        with torch.cuda.stream(s):
-            lvlip.batch_torch(base, descs, o, kernel=lvlip.KERNEL_WAVE_DYN, waves_per_cu=1,
-                              stream=s, len_hint=hint)
-    torch.cuda.synchronize()
-    for i, o in enumerate(outs):
-        assert np.array_equal(o.cpu().numpy().view(np.uint16), want), i
-    # graph capture (a block of its own), replayed twice, then a direct launch
-    out.zero_()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_WAVE_DYN, waves_per_cu=1,
-                          stream=torch.cuda.current_stream(), len_hint=hint)
-    for _ in range(2):
-        out.zero_()
-        g.replay()
-        torch.cuda.synchronize()
-        assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
-    lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_WAVE_DYN, waves_per_cu=1, len_hint=hint)
-    torch.cuda.synchronize()
-    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
-    del g
-
-
-@pytest.mark.parametrize("name,n", [("tcp1500", 300000), ("tcp9000", 100000), ("mixed", 150000)])
-def test_stream_slot_weights_relaunch(name, n):
-    """The slot weights (FB, LVLIP_STREAM_FB=1 in a child process: the knob is
-    read once per process) change from launch to launch on one stream (and
-    start over on a new stream): every launch must stay bit-exact, and so must
-    a graph replay and a second stream running at the same time."""
-    import subprocess
-    import sys
-    if os.environ.get("LVLIP_STREAM_FB") != "1":
-        env = dict(os.environ, LVLIP_STREAM_FB="1")
-        r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
-                            f"{__file__}::test_stream_slot_weights_relaunch[{name}-{n}]"],
-                           env=env, capture_output=True, text=True, timeout=600)
-        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-        return
+@pytest.mark.parametrize("name,n,kernel,unroll,wpc", [
+    ("tcp1500", 300000, lvlip.KERNEL_AUTO, 0, 0), ("tcp9000", 100000, lvlip.KERNEL_AUTO, 0, 0),
+    ("mixed", 150000, lvlip.KERNEL_AUTO, 0, 0), ("tcp1500", 300000, lvlip.KERNEL_WAVE, 3, 8),
+    ("mixed", 150000, lvlip.KERNEL_WINDOW, 2 | (4 << 8), 16)])
+def test_relaunch_streams_and_graph(name, n, kernel, unroll, wpc):
+    """Back-to-back launches on one stream, six launches spread over two streams
+    running at the same time, and a HIP-graph replay: every run bit-exact (the
+    ring kernels keep no state across launches; nothing is shared between
+    concurrent launches but the read-only batch)."""
     b = workloads.make(name, n=n)
     base, descs, out = workloads.to_device(b)
     hint = b.algo_bytes // b.n
     want = pyoracle.batch(base.cpu().numpy(), b.descs, threads=THREADS)
-    for rep in range(12):
+
+    def launch(o, st):
+        lvlip.batch_torch(base, descs, o, kernel=kernel, unroll=unroll, waves_per_cu=wpc,
+                          stream=st, len_hint=hint)
+    for rep in range(6):
         out.fill_(0)
-        lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_WAVE, len_hint=hint)
+        launch(out, torch.cuda.current_stream())
         torch.cuda.synchronize()
         got = out.cpu().numpy().view(np.uint16)
         bad = np.nonzero(got != want)[0]
@@ -543,14 +488,13 @@ def test_stream_slot_weights_relaunch(name, n):
     for i, o in enumerate(outs):
         st = s1 if i % 2 == 0 else s2
         with torch.cuda.stream(st):
-            lvlip.batch_torch(base, descs, o, kernel=lvlip.KERNEL_WAVE, stream=st, len_hint=hint)
+            launch(o, st)
     torch.cuda.synchronize()
     for i, o in enumerate(outs):
         assert np.array_equal(o.cpu().numpy().view(np.uint16), want), i
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        lvlip.batch_torch(base, descs, out, kernel=lvlip.KERNEL_WAVE,
-                          stream=torch.cuda.current_stream(), len_hint=hint)
+        launch(out, torch.cuda.current_stream())
     for _ in range(3):
         out.zero_()
         g.replay()

@@ -35,7 +35,9 @@ def asm():
 
 
 def functions(text):
-    """name -> list of instruction lines (comments/labels/directives dropped)."""
+    """name -> list of instruction lines (comments/labels/directives dropped),
+    from the function's label to its .Lfunc_end marker (a kernel with an early
+    return has more than one s_endpgm)."""
     funcs, cur, name = {}, None, None
     for line in text.splitlines():
         m = re.match(r"^(_Z\w+):", line)
@@ -45,38 +47,24 @@ def functions(text):
             continue
         if cur is None:
             continue
+        if line.startswith(".Lfunc_end"):
+            cur = None
+            continue
         s = line.split(";")[0].strip()
         if not s or s.startswith(".") or s.endswith(":"):
-            if "s_endpgm" in line:
-                cur = None
             continue
         cur.append(s)
-        if s.startswith("s_endpgm"):
-            cur = None
     return funcs
 
 
-def flags(name):
-    """(DYN, FB) template flags of a mangled k_stream<R, POL, DYN, FB> name."""
-    m = re.search(r"k_streamILi\d+ELi\d+ELb([01])ELb([01])E", name)
-    return (m.group(1) == "1", m.group(2) == "1") if m else (False, False)
-
-
-def is_dyn(name):
-    return flags(name)[0]
-
-
-def is_fb(name):
-    return flags(name)[1]
-
-
 def stream_kernels(asm):
-    """k_stream and k_window instantiations (the ring kernels)."""
+    """k_stream and k_window instantiations (the ring kernels, one body)."""
     f = functions(asm)
     ks = {n: body for n, body in f.items() if "k_stream" in n or "k_window" in n}
-    assert any("k_stream" in n for n in ks), "no k_stream instantiations found"
-    assert any(is_dyn(n) for n in ks), "no k_stream<.., DYN = true> instantiations found"
-    assert any(is_fb(n) for n in ks), "no k_stream<.., FB = true> instantiations found"
+    # k_stream<R, POL>: 2-4 pieces in flight, the five load policies
+    st = {tuple(int(x) for x in re.search(r"k_streamILi(\d+)ELi(\d+)E", n).groups())
+          for n in ks if "k_stream" in n}
+    assert st == {(r, p) for r in (2, 3, 4) for p in range(5)}, sorted(st)
     # k_window<R, G>: every pieces-in-flight x group-size pair the launcher uses
     win = {tuple(int(x) for x in re.search(r"k_windowILi(\d+)ELi(\d+)E", n).groups())
            for n in ks if "k_window" in n}
@@ -116,49 +104,16 @@ def test_lds_dma_m0_sequence(asm):
 
 def test_ring_waits_are_counted_not_draining(asm):
     for name, body in stream_kernels(asm).items():
-        if is_dyn(name):
-            continue  # test_dyn_streamers_never_drain
         r = pieces(name)
         waits = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt" in ins]
         ring = [w for w in waits if f"vmcnt({2 * (r - 1)})" in w]
         assert len(ring) == r, (name, waits)
-        # one drain after the first window fill, one before s_endpgm; FB adds
-        # the waits of its system-coherent weight loads at the start (each
-        # right after its load) and of its exit atomic
-        drains = 0
-        for i, ins in enumerate(body):
-            if ins.startswith("s_waitcnt") and "vmcnt(0)" in ins:
-                prev = body[i - 1]
-                if is_fb(name) and prev.startswith("global_load_dword") and "sc0 sc1" in prev:
-                    continue
-                drains += 1
-        assert drains <= (3 if is_fb(name) else 2), (name, waits)
+        # one drain after the first window fill, one before s_endpgm
+        drains = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt(0)" in ins]
+        assert len(drains) <= 2, (name, waits)
 
 
 def test_no_scratch(asm):
     for m in re.finditer(r"\.name:\s+(_Z\w*k_(?:stream|window)\w*)\n(?:.*\n){0,60}?\s+\.private_segment_fixed_size:\s+(\d+)",
                          asm):
         assert int(m.group(2)) == 0, m.group(1)
-
-
-def test_dyn_streamers_never_drain(asm):
-    """k_stream with DYN: the streamers keep the counted ring waits; the only
-    draining waits are the first window fill(s), the streamer exit and the
-    claimer's own waits on its atomics (a global atomic or the sc0 sc1 mask
-    read shortly before).  No AGPRs."""
-    for name, body in stream_kernels(asm).items():
-        if not is_dyn(name):
-            continue
-        r = pieces(name)
-        waits = [ins for ins in body if ins.startswith("s_waitcnt") and "vmcnt" in ins]
-        assert sum(f"vmcnt({2 * (r - 1)})" in w for w in waits) >= r, (name, waits)
-        other = 0
-        for i, ins in enumerate(body):
-            if ins.startswith("s_waitcnt") and "vmcnt(0)" in ins:
-                near = body[max(0, i - 12):i]
-                claimer = any(x.startswith("global_atomic") or
-                              (x.startswith("global_load_dword") and "sc0 sc1" in x) for x in near)
-                if not claimer:
-                    other += 1
-        assert other <= 4, (name, other)
-        assert not any(re.search(r"\ba\[?\d+", ins) for ins in body), name
