@@ -12,25 +12,27 @@
 // adds is exact (mod-2^32 addition is associative); end-around-carry folding is
 // applied once, after the seed, exactly as the reference does.
 //
-// Byte alignment: the GPU reads whole 16-byte aligned chunks covering
+// Byte alignment (the flat and round-1 kernels; the ring kernels read through a
+// per-packet buffer resource whose base is the packet's first byte instead, so
+// their words are packet-relative, see below): the GPU reads whole 16-byte aligned chunks covering
 // [offset, offset+len) and zeroes the bytes outside the packet.  When offset is
 // odd, each aligned u16 holds (odd-relative byte, even-relative byte), so the
 // two bytes of every half-dword are swapped before summing; the reference's
 // tail byte (even relative index) then lands in the low byte as it should.
 //
-// Kernels (roofline: HBM read bandwidth; ~1 VALU op per loaded dword, no MFMA):
-//   k_wave  : one wavefront per packet (BASELINE.json north_star).  A wave's 64
-//             lanes read consecutive 16-B chunks of its packet (1 KiB per
-//             instruction, fully coalesced), U instructions in flight per lane,
-//             then a 64-lane u32 reduction and the fold on lane 0.
-//   k_wave_lds : the same, but the chunks are staged HBM -> LDS by LDS-DMA
-//             (global_load_lds_dwordx4) and read back with ds_read_b128.
-//   k_flat  : chunk-balanced tile sweep for ragged batches.  A 256-thread
-//             workgroup owns 256 descriptors; their chunk counts are prefix-summed
-//             in LDS, every lane takes one chunk per step (coalesced across packet
-//             boundaries), a segmented wave reduction keyed by descriptor index
-//             merges lanes of one packet, and the segment tails add into per-
-//             descriptor u32 accumulators in LDS.  No lane idles on 20-B headers.
+// Kernels (roofline: HBM read bandwidth; ~1 VALU op per loaded dword, no MFMA;
+// DESIGN.md §4):
+//   k_window  : the default from 512 B.  One wavefront per packet, persistent, a
+//               ring of 2-KiB pieces in flight per wave; packets dealt to the
+//               waves in small groups round robin over the grid, so the waves in
+//               flight read one narrow window of the batch.
+//   k_stream  : the same ring with contiguous per-wave ranges (A/B).
+//   k_flat2   : the default below 512 B (ragged batches: 20-B headers next to
+//               payloads).  A chunk-balanced tile sweep over 16-B chunks that
+//               crosses packet boundaries; segment sums by a DPP prefix scan.
+//               Also the frame calls' kernel (flat_src.h, skb_dev.hip).
+//   k_wflat   : k_flat2's sweep one wave per tile, tiles dealt round robin (A/B).
+//   k_wave_simple, k_wave_lds, k_flat : round-1 variants kept for A/B.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
