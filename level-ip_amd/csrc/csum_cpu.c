@@ -65,6 +65,8 @@ static uint32_t sum_words_scalar(const uint8_t *p, int count)
  * mod 2^32, which is exactly the reference's arithmetic, so no flushing. */
 __attribute__((target("avx2"))) static uint32_t sum_words_avx2(const uint8_t *p, int count)
 {
+    if (count < 64) /* IPv4 headers and other short buffers: no vector setup */
+        return sum_words_scalar(p, count);
     const __m256i z = _mm256_setzero_si256();
     __m256i a0 = z, a1 = z, a2 = z, a3 = z;
     while (count >= 64) {
@@ -85,19 +87,71 @@ __attribute__((target("avx2"))) static uint32_t sum_words_avx2(const uint8_t *p,
         s += lanes[i];
     return s + sum_words_scalar(p, count);
 }
+
+/* AVX-512: 128 bytes per step.  Each u32 lane of a 64-B vector holds two
+ * words; the low one (and with 0xffff) and the high one (shift by 16) are added
+ * into u32 lanes, which wrap mod 2^32 like the reference's sum.  On Zen 5 (the
+ * MI355X hosts' EPYC 9575F) the 512-bit datapath is full width. */
+__attribute__((target("avx512f,avx512bw,avx2"))) static uint32_t sum_words_avx512(const uint8_t *p,
+                                                                                int count)
+{
+    const __m512i lo16 = _mm512_set1_epi32(0xffff);
+    __m512i a0 = _mm512_setzero_si512(), a1 = _mm512_setzero_si512();
+    while (count >= 128) {
+        const __m512i v0 = _mm512_loadu_si512((const void *)p);
+        const __m512i v1 = _mm512_loadu_si512((const void *)(p + 64));
+        a0 = _mm512_add_epi32(a0, _mm512_add_epi32(_mm512_and_si512(v0, lo16), _mm512_srli_epi32(v0, 16)));
+        a1 = _mm512_add_epi32(a1, _mm512_add_epi32(_mm512_and_si512(v1, lo16), _mm512_srli_epi32(v1, 16)));
+        p += 128;
+        count -= 128;
+    }
+    if (count >= 64) {
+        const __m512i v0 = _mm512_loadu_si512((const void *)p);
+        a0 = _mm512_add_epi32(a0, _mm512_add_epi32(_mm512_and_si512(v0, lo16), _mm512_srli_epi32(v0, 16)));
+        p += 64;
+        count -= 64;
+    }
+    if (count > 0) {
+        /* the last 1..63 bytes in one masked load: masked-off bytes read as 0 and
+         * are never accessed (no fault past the buffer), so an odd last byte is
+         * the low byte of a word whose high byte is 0, as utils.c:34-35 adds it */
+        const __m512i v = _mm512_maskz_loadu_epi8((__mmask64)((1ull << count) - 1ull), (const void *)p);
+        a1 = _mm512_add_epi32(a1, _mm512_add_epi32(_mm512_and_si512(v, lo16), _mm512_srli_epi32(v, 16)));
+    }
+    /* lane sum in vector (wrapping) adds and unsigned scalars: the compiler's
+     * _mm512_reduce_add_epi32 sums in int, which overflows (UB) here */
+    const __m512i a = _mm512_add_epi32(a0, a1);
+    const __m256i h = _mm256_add_epi32(_mm512_castsi512_si256(a), _mm512_extracti64x4_epi64(a, 1));
+    uint32_t lanes[8];
+    _mm256_storeu_si256((__m256i *)(void *)lanes, h);
+    uint32_t t = 0;
+    for (int i = 0; i < 8; i++)
+        t += lanes[i];
+    return t;
+}
 #endif
 
 typedef uint32_t (*sum_fn)(const uint8_t *, int);
 static sum_fn g_sum; /* chosen once; racing first callers store the same value */
 
+/* The widest path the CPU has.  LVLIP_CPU_SUM=scalar|avx2|avx512 caps it (A/B
+ * and tests); LVLIP_CPU_SCALAR=1 is the older spelling of "scalar". */
 static sum_fn pick_sum(void)
 {
     sum_fn f = sum_words_scalar;
 #if defined(__x86_64__)
+    const char *cap = getenv("LVLIP_CPU_SUM");
     const char *force = getenv("LVLIP_CPU_SCALAR");
+    int level = 2; /* 0 scalar, 1 avx2, 2 avx512 */
+    if ((force && force[0] == '1') || (cap && !strcmp(cap, "scalar")))
+        level = 0;
+    else if (cap && !strcmp(cap, "avx2"))
+        level = 1;
     __builtin_cpu_init();
-    if (!(force && force[0] == '1') && __builtin_cpu_supports("avx2"))
+    if (level >= 1 && __builtin_cpu_supports("avx2"))
         f = sum_words_avx2;
+    if (level >= 2 && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw"))
+        f = sum_words_avx512;
 #endif
     __atomic_store_n(&g_sum, f, __ATOMIC_RELAXED);
     return f;

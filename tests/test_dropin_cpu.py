@@ -4,6 +4,7 @@ the reference stack with a fake TAP, CPU only)."""
 import ctypes
 
 import numpy as np
+import pytest
 
 import golden_io
 import lvlip
@@ -156,24 +157,42 @@ def test_sum_every_alignment_and_length():
             assert lvlip.sum_every_16bits(a if ln else b"\0", ln) == _word_sum(a, ln), (off, ln)
 
 
-def test_portable_loop_forced():
-    """LVLIP_CPU_SCALAR=1 selects the portable loop; same results (subprocess:
-    the choice is made once per process)."""
+def _cpu_flags():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    return set(line.split(":", 1)[1].split())
+    except OSError:
+        pass
+    return set()
+
+
+@pytest.mark.parametrize("path", ["scalar", "avx2", "avx512"])
+def test_each_sum_path(path):
+    """LVLIP_CPU_SUM caps the per-call word sum at the portable loop, AVX2 or
+    AVX-512 (masked-load tail); every path gives the same results at every
+    length 0-299 and 16 alignments (subprocess: the choice is made once per
+    process).  A path the CPU lacks is skipped."""
     import os
     import subprocess
     import sys
+
+    need = {"scalar": set(), "avx2": {"avx2"}, "avx512": {"avx512f", "avx512bw"}}[path]
+    if not need <= _cpu_flags():
+        pytest.skip(f"CPU lacks {sorted(need)}")
 
     code = (
         "import sys; sys.path.insert(0, %r)\n"
         "import numpy as np, lvlip\n"
         "rng = np.random.default_rng(5); b = rng.integers(0, 256, 300000, dtype=np.uint8)\n"
         "for off in range(17):\n"
-        "  for ln in (0, 1, 15, 16, 17, 63, 64, 65, 1500, 262145, 299000):\n"
+        "  for ln in list(range(0, 300)) + [1500, 9000, 262145, 299000]:\n"
         "    a = b[off:off + ln]\n"
         "    w = int(a[: ln & ~1].view('<u2').astype(np.uint64).sum()) + (int(a[-1]) if ln & 1 else 0)\n"
         "    assert lvlip.sum_every_16bits(a if ln else b'\\0', ln) == w & 0xFFFFFFFF, (off, ln)\n"
         "print('ok')\n" % os.path.dirname(lvlip.__file__))
-    env = dict(os.environ, LVLIP_CPU_SCALAR="1")
+    env = dict(os.environ, LVLIP_CPU_SUM=path)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr

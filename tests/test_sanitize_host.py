@@ -3,7 +3,7 @@ level-ip's `make debug` is a -fsanitize=thread build, Makefile:17-18, and its
 runner greps ThreadSanitizer reports, tests/test-run-all:41).
 
 tests/sanitize/host_san.c drives level-ip_amd/csrc/csum_cpu.c (the per-call
-drop-in, AVX2 and portable paths) and level-ip_amd/csrc/skb_batch.c (the frame
+drop-in, AVX-512, AVX2 and portable paths) and level-ip_amd/csrc/skb_batch.c (the frame
 calls' multi-threaded host steps) against the oracle; see its header.  Host
 code only: GPU sanitizers are not available on the MI355X pool."""
 import os
@@ -44,10 +44,10 @@ def _check(r):
     assert "all checks passed" in r.stdout
 
 
-@pytest.mark.parametrize("scalar", ["0", "1"])
-def test_host_code_asan_ubsan(tmp_path, scalar):
+@pytest.mark.parametrize("path", ["avx512", "avx2", "scalar"])
+def test_host_code_asan_ubsan(tmp_path, path):
     exe = _build("asan", tmp_path)
-    env = dict(os.environ, LVLIP_CPU_SCALAR=scalar)
+    env = dict(os.environ, LVLIP_CPU_SUM=path)  # capped: the CPU may lack the wider ones
     _check(subprocess.run([exe], capture_output=True, text=True, env=env, timeout=600))
 
 
