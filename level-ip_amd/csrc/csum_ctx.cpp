@@ -133,6 +133,20 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
     return LVLIP_OK;
 }
 
+// End of a batch call: hand over the results still in flight.  After a
+// failure, also wait for whatever a half-enqueued piece left on the slot
+// streams (an H2D copy from the pinned arena, say), so that the next call can
+// reuse the arenas and the caller's buffers are no longer read.
+int finish_pieces(lvlip_csum_ctx* c, int rc) {
+    for (auto& s : c->slot) {
+        const int r2 = drain(c, s);
+        if (rc == LVLIP_OK) rc = r2;
+    }
+    if (rc != LVLIP_OK)
+        for (auto& s : c->slot) (void)hipStreamSynchronize(s.stream);
+    return rc;
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -198,11 +212,7 @@ int zerocopy_batch(lvlip_csum_ctx* c, const Region& r, uint32_t n, uint16_t* out
         rc = launch_piece(c, s, bytes ? bytes : 16, k, out + first, nullptr, d0);
         cur ^= 1;
     }
-    for (auto& s : c->slot) {
-        const int r2 = drain(c, s);
-        if (rc == LVLIP_OK) rc = r2;
-    }
-    return rc;
+    return finish_pieces(c, rc);
 }
 
 }  // namespace
@@ -372,11 +382,7 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
         rc = launch_piece(c, s, off ? off : 16, k, out + first);
         cur ^= 1;
     }
-    for (auto& s : c->slot) {
-        const int r2 = drain(c, s);
-        if (rc == LVLIP_OK) rc = r2;
-    }
-    return rc;
+    return finish_pieces(c, rc);
 }
 
 int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_bytes,
@@ -442,11 +448,7 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
         rc = launch_piece(c, s, span ? span : 16, k, out + first, from);
         cur ^= 1;
     }
-    for (auto& s : c->slot) {
-        const int r2 = drain(c, s);
-        if (rc == LVLIP_OK) rc = r2;
-    }
-    return rc;
+    return finish_pieces(c, rc);
 }
 
 }  // extern "C"
