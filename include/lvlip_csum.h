@@ -144,7 +144,10 @@ typedef struct lvlip_launch_cfg {
                                wave; WINDOW: | packets per group << 8
                                (1, 2, 3, 4 or 8; 0 = by len_hint);
                                WFLAT: 64-chunk loads per round | descriptors
-                               per tile << 8 (16, 32 or 64; 0 = 32)          */
+                               per tile << 8 (16, 32 or 64; 0 = 32);
+                               FLAT: 64-chunk loads per round | group order
+                               << 8 (1 interleaved, 2 quarters, 3 blocks;
+                               0 = LVLIP_FLAT_GROUPS, else quarters)         */
     int32_t  waves_per_cu;  /* WAVE: resident waves per CU (0 = 8); others:
                                grid cap (0 = one wave per packet)           */
     int32_t  len_hint;      /* average packet length in bytes if the caller

@@ -825,7 +825,7 @@ __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
     return ((1u << w) - 1u) << (8 * s);
 }
 
-template <int U, bool NT, bool CONTIG, class Src>
+template <int U, bool NT, int GORD, class Src>
 __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, const Src src,
                                               uint32_t n) {
     __shared__ uint4 s_rec[FT];        // by rank: {a0 lo, a0 hi, cstart, meta}
@@ -907,17 +907,21 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
     // segment that starts at lane 0 as a continuation needs nothing (exclusive
     // prefix 0).  One LDS atomic per group carries both.
     //
-    // Group order: wave w takes groups [w*G/4, (w+1)*G/4) in rounds of U
-    // consecutive groups (CONTIG), so the 128-B line two neighbouring groups
-    // share is requested twice back to back by one wave, and merges in L2,
-    // instead of by two waves at different times (PMC: 4.4 % re-fetched lines
-    // with the interleaved order).
-    const uint32_t gstep = CONTIG ? 1u : 4u;
+    // Group order (GORD).  2 (default) = blocks: a round of the workgroup is 4U
+    // consecutive groups, U per wave, so the tile is read as one stream and
+    // only every U-th group boundary (a 128-B line two groups can share) falls
+    // between two waves, which request it at about the same time.  1 = quarters:
+    // wave w takes groups [w*G/4, (w+1)*G/4), four streams per tile.  0 =
+    // interleaved, groups w, w+4, ...: every shared line is requested by two
+    // waves at different times (PMC: 4.4 % re-fetched lines).  Blocks against
+    // quarters on mixed: +0.5-1.6 % (U 8 / U 4) and 0.9 % less HBM traffic.
+    const uint32_t gstep = GORD == 0 ? 4u : 1u;             // between a round's groups
+    const uint32_t rstep = GORD == 1 ? (uint32_t)U : 4u * U;  // between rounds
     const uint32_t gper = (G + 3u) / 4u;
-    const uint32_t g_lo = CONTIG ? wid * gper : wid;
-    const uint32_t g_end = CONTIG ? (g_lo + gper < G ? g_lo + gper : G) : G;
+    const uint32_t g_lo = GORD == 1 ? wid * gper : (GORD == 2 ? wid * (uint32_t)U : wid);
+    const uint32_t g_end = GORD == 1 ? (g_lo + gper < G ? g_lo + gper : G) : G;
     if (C > 0) {
-        for (uint32_t gr = g_lo; gr < g_end; gr += gstep * U) {
+        for (uint32_t gr = g_lo; gr < g_end; gr += rstep) {
             uint4 x[U];
             uint32_t mt[U], kk[U];
             bool vl[U];
@@ -1379,12 +1383,16 @@ int load_policy() {
 }
 bool load_nt() { return load_policy() != 1; }
 
-// LVLIP_FLAT_GROUPS=interleaved (A/B knob): k_flat2's waves take groups
-// w, w+4, ... instead of contiguous quarters of the tile.
-bool flat_contig() {
-    static const bool c = [] {
+// LVLIP_FLAT_GROUPS (A/B knob, read once): k_flat2's group order.
+// block (default, 2: rounds of 4U consecutive groups, U per wave) | quarters
+// (1: contiguous quarters of the tile per wave, round 1's order) | interleaved
+// (0: groups w, w+4, ...; batch calls only).
+int flat_group_order() {
+    static const int c = [] {
         const char* e = getenv("LVLIP_FLAT_GROUPS");
-        return !(e && strcmp(e, "interleaved") == 0);
+        if (e && strcmp(e, "interleaved") == 0) return 0;
+        if (e && strcmp(e, "quarters") == 0) return 1;
+        return 2;
     }();
     return c;
 }
@@ -1585,8 +1593,12 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         case LVLIP_KERNEL_WINDOW: {
             // unroll = 2-KiB pieces in flight per wave (low byte, default 3) |
             // packets per group << 8 (0 = by len_hint); 8 waves/CU by default
-            const int group = unroll > 0 ? (unroll >> 8) & 0xff : 0;
-            int r = unroll > 0 ? unroll & 0xff : 0;
+            if (unroll < 0) unroll = 0;
+            const int group = (unroll >> 8) & 0xff;
+            if ((unroll >> 16) != 0 ||
+                (group != 0 && group != 1 && group != 2 && group != 3 && group != 4 && group != 8))
+                return LVLIP_EINVAL;
+            int r = unroll & 0xff;
             if (r == 0) r = 3;
             const int w = wpc > 0 ? wpc : 8;
             const int hint = cfg ? cfg->len_hint : 0;
@@ -1643,23 +1655,27 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             // 8 loads of 64 chunks per round: 94 VGPRs, 5 workgroups per CU with
             // 8 KiB in flight per wave; 2-3 % ahead of 4 (8 workgroups, 4 KiB)
             // on mixed in 3 of 4 same-process A/B runs
+            if (unroll < 0) unroll = 0;
+            if ((unroll >> 10) != 0) return LVLIP_EINVAL;
+            const int uo = (unroll >> 8) & 3;  // group order + 1 (A/B), 0 = the knob's
+            unroll &= 0xFF;
             if (unroll <= 0) unroll = 8;
             const bool nt = load_nt();
-            const bool contig = flat_contig();
-            switch (unroll * 4 + (nt ? 2 : 0) + (contig ? 1 : 0)) {
+            const int gord = uo ? uo - 1 : flat_group_order();
+            switch (unroll * 8 + (nt ? 4 : 0) + gord) {
 #define LVLIP_FLAT(UU, NTV, CG)                                                               \
-    case UU * 4 + (NTV ? 2 : 0) + (CG ? 1 : 0):                                              \
+    case UU * 8 + (NTV ? 4 : 0) + CG:                                                        \
         hipLaunchKernelGGL((lvlip::k_flat2<UU, NTV, CG, lvlip::DescSrc>), dim3(grid),         \
                            dim3(lvlip::FT), flat_lds_pad(), s, (const uint8_t*)base,         \
                            lvlip::DescSrc{descs, out}, n);                                  \
         break;
-                LVLIP_FLAT(2, true, true) LVLIP_FLAT(2, true, false)
-                LVLIP_FLAT(2, false, true) LVLIP_FLAT(2, false, false)
-                LVLIP_FLAT(4, true, true) LVLIP_FLAT(4, true, false)
-                LVLIP_FLAT(4, false, true) LVLIP_FLAT(4, false, false)
-                LVLIP_FLAT(8, true, true) LVLIP_FLAT(8, true, false)
-                LVLIP_FLAT(8, false, true) LVLIP_FLAT(8, false, false)
-                LVLIP_FLAT(6, true, true) LVLIP_FLAT(12, true, true)
+                LVLIP_FLAT(2, true, 1) LVLIP_FLAT(2, true, 0) LVLIP_FLAT(2, true, 2)
+                LVLIP_FLAT(2, false, 1) LVLIP_FLAT(2, false, 0) LVLIP_FLAT(2, false, 2)
+                LVLIP_FLAT(4, true, 1) LVLIP_FLAT(4, true, 0) LVLIP_FLAT(4, true, 2)
+                LVLIP_FLAT(4, false, 1) LVLIP_FLAT(4, false, 0) LVLIP_FLAT(4, false, 2)
+                LVLIP_FLAT(8, true, 1) LVLIP_FLAT(8, true, 0) LVLIP_FLAT(8, true, 2)
+                LVLIP_FLAT(8, false, 1) LVLIP_FLAT(8, false, 0) LVLIP_FLAT(8, false, 2)
+                LVLIP_FLAT(6, true, 1) LVLIP_FLAT(6, true, 2) LVLIP_FLAT(12, true, 1) LVLIP_FLAT(12, true, 2)
 #undef LVLIP_FLAT
                 default: return LVLIP_EINVAL;
             }
@@ -1721,6 +1737,18 @@ int frames_unroll() {
     return v;
 }
 
+// LVLIP_FRAMES_GROUPS (A/B knob, read once): the frame calls' k_flat2 group
+// order, quarters (default) | block.  Blocks measured 7-9 % slower on the RX
+// header call (20-B pieces, 0.090 vs 0.084 ms) and within 1 % on TX fill and
+// RX + L4, so the frame calls keep quarters.
+bool frames_quarters() {
+    static const bool q = [] {
+        const char* e = getenv("LVLIP_FRAMES_GROUPS");
+        return !(e && strcmp(e, "block") == 0);
+    }();
+    return q;
+}
+
 template <int MODE>
 int launch_frames(const void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* out8,
                   hipStream_t s) {
@@ -1732,12 +1760,16 @@ int launch_frames(const void* base, const lvlip_frame_desc* frames, uint32_t n, 
         const uint32_t entries = m * Src::SLOTS;
         const uint32_t grid = (uint32_t)(((uint64_t)entries + lvlip::FT - 1) / lvlip::FT);
         Src src{(const uint8_t*)base, (uint8_t*)base, frames + f0, out8 ? out8 + f0 : nullptr};
-        if (frames_unroll() == 8)
-            hipLaunchKernelGGL((lvlip::k_flat2<8, true, true, Src>), dim3(grid), dim3(lvlip::FT), 0, s,
-                               (const uint8_t*)base, src, entries);
-        else
-            hipLaunchKernelGGL((lvlip::k_flat2<4, true, true, Src>), dim3(grid), dim3(lvlip::FT), 0, s,
-                               (const uint8_t*)base, src, entries);
+        const bool quarters = frames_quarters();
+#define LVLIP_FRAMES_K(UU, GO)                                                              \
+    hipLaunchKernelGGL((lvlip::k_flat2<UU, true, GO, Src>), dim3(grid), dim3(lvlip::FT), 0, s, \
+                       (const uint8_t*)base, src, entries)
+        if (frames_unroll() == 8) {
+            if (quarters) LVLIP_FRAMES_K(8, 1); else LVLIP_FRAMES_K(8, 2);
+        } else {
+            if (quarters) LVLIP_FRAMES_K(4, 1); else LVLIP_FRAMES_K(4, 2);
+        }
+#undef LVLIP_FRAMES_K
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "k_flat2 (frames)");
         f0 += m;

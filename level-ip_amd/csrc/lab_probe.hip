@@ -126,6 +126,7 @@ __global__ __launch_bounds__(256) void k_probe(const uint4* __restrict__ src, ui
 // `cp` consecutive 1 KiB pieces (cp a multiple of U); wave w owns chunks
 // w, w + nw, ... and walks each one U pieces (U KiB in flight) at a time.
 // The window the waves in flight cover is nw * cp KiB.
+// order 2: block-level chunks, see below.
 // order 1 numbers the waves XCD-major (block b sits on XCD b % 8 as observed;
 // grid a multiple of 8), so consecutive chunks stay on one XCD.
 template <int U>
@@ -139,6 +140,25 @@ __global__ __launch_bounds__(256) void k_probe_chunk(const uint4* __restrict__ s
     const uint64_t pieces = n16 / 64;
     const uint64_t nw = (uint64_t)gridDim.x * wpb;
     const uint64_t chunks = pieces / cp;
+    if (order == 2) {
+        // block chunks (k_flat2's tile sweep in block order): block b owns chunks
+        // b, b + grid, ...; its waves take U-piece slices of a chunk round robin,
+        // so a block is one stream of 4U KiB per round, cp KiB long
+        for (uint64_t c = blockIdx.x; c < chunks; c += gridDim.x) {
+            for (uint32_t q = wid * U; q < cp; q += wpb * U) {
+                uint4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) v[u] = ld<true>(src + (c * cp + q + u) * 64 + lane);
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc += words(v[u]);
+            }
+        }
+        for (uint64_t p = chunks * cp + (uint64_t)blockIdx.x * wpb + wid; p < pieces; p += nw)
+            acc += words(ld<true>(src + p * 64 + lane));
+        acc = wsum(acc);
+        if (lane == 0) atomicAdd(sink, acc);
+        return;
+    }
     const uint64_t rank = order ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * wpb + wid
                                 : (uint64_t)blockIdx.x * wpb + wid;
     for (uint64_t c = rank; c < chunks; c += nw) {
@@ -349,7 +369,7 @@ extern "C" int lvlip_lab_probe(const void* src, uint64_t bytes, uint32_t* sink, 
 extern "C" int lvlip_lab_probe_chunk(const void* src, uint64_t bytes, uint32_t* sink, int unroll,
                                      uint32_t chunk_pieces, uint32_t order, int blocks, void* stream) {
     if (!src || !sink || (bytes & 1023u) || chunk_pieces == 0 || chunk_pieces % (uint32_t)unroll ||
-        (order && (blocks & 7)))
+        (order == 1 && (blocks & 7)) || order > 2 || (order == 2 && chunk_pieces % (4u * (uint32_t)unroll)))
         return -1;
     hipStream_t s = (hipStream_t)stream;
     const dim3 g((uint32_t)blocks), b(256);

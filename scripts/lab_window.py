@@ -6,6 +6,7 @@ Probe modes (level-ip_amd/csrc/lab_probe.hip), all nontemporal 16-B/lane loads:
   m1  block-contiguous ranges
   m2  wave-contiguous ranges (k_stream's layout: nw far-apart streams)
   m5  chip-wide window (wave w reads U-KiB chunks w, w+nw, ...)
+  c   chunk probe: order 0/1 wave chunks (window when small), order 2 block chunks
 Interleaved rounds in one process; prints the median GB/s per variant.
 
   LAB_WORKLOAD=tcp1500 python scripts/lab_window.py [out.json]
@@ -68,6 +69,16 @@ def main():
         # the mixed buffer: window vs contiguous orders at 8 and 32 waves/CU
         variants += [("c", 4, 4, 1, 2), ("c", 4, 4, 1, 8), ("c", 4, 16, 1, 8), ("c", 8, 8, 1, 4),
                      (2, 8, 0, 0, 2), (2, 4, 0, 0, 8), (1, 8, 0, 0, 2), (1, 4, 0, 0, 8)]
+    elif lab_set == "blockchunk":
+        # k_flat2-like block streams on the mixed buffer: block chunks of cp KiB
+        # (the tile's bytes), 4 waves taking U-KiB slices round robin, bpc blocks
+        # per CU; against the chip-wide window and contiguous wave ranges
+        for cp in (32, 64, 128, 256):
+            for bpc in (2, 5, 8):
+                variants.append(("c", 8, cp, 2, bpc))
+        for cp in (16, 32, 64, 128):
+            variants.append(("c", 4, cp, 2, 5))
+        variants += [("c", 4, 4, 1, 2), ("c", 8, 8, 1, 2), (2, 8, 0, 0, 2), (2, 8, 0, 0, 5), (1, 8, 0, 0, 5)]
     elif lab_set == "pkwin":
         # group g: two loads per slot; 100 + g: the group's span in whole loads
         for g in (1, 2, 3, 4, 6, 8, 101, 102, 103, 104, 106, 108):

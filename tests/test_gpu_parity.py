@@ -40,6 +40,9 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT, 8, 0),
     (lvlip.KERNEL_FLAT, 6, 0),
     (lvlip.KERNEL_FLAT, 12, 0),
+    (lvlip.KERNEL_FLAT, 4 | (1 << 8), 0),  # group orders: interleaved, quarters, blocks
+    (lvlip.KERNEL_FLAT, 8 | (2 << 8), 0),
+    (lvlip.KERNEL_FLAT, 2 | (3 << 8), 0),
     (5, 0, 0),                     # first-generation flat kernel (A/B)
     (lvlip.KERNEL_WINDOW, 3, 0),   # interleaved stream: groups dealt round robin
     (lvlip.KERNEL_WINDOW, 2, 1),   # 1 wave/CU: long per-wave sequences, window refills
@@ -334,6 +337,17 @@ def test_misaligned_base_rejected():
     out = torch.empty(1, dtype=torch.int16, device="cuda")
     with pytest.raises(lvlip.LvlipError):
         lvlip.batch_dev(base.data_ptr() + 2, descs.data_ptr(), 1, out.data_ptr())
+
+
+def test_bad_launch_shapes_rejected():
+    """Shapes no kernel is built for return LVLIP_EINVAL (nothing launched)."""
+    base = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    descs = dev_descs(mk_descs([0], [4], [0]))
+    out = torch.empty(1, dtype=torch.int16, device="cuda")
+    for k, u in ((lvlip.KERNEL_FLAT, 3), (lvlip.KERNEL_FLAT, 8 | (4 << 8)),
+                 (lvlip.KERNEL_WINDOW, 2 | (5 << 8)), (lvlip.KERNEL_WFLAT, 8 | (48 << 8))):
+        with pytest.raises(lvlip.LvlipError):
+            lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None, k, u, 0, 0)
 
 
 # ----------------------------------------------------------- host batches --
