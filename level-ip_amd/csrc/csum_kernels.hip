@@ -1554,9 +1554,10 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
     int unroll = cfg ? cfg->unroll : 0;
     int wpc = cfg ? cfg->waves_per_cu : 0;
     if (kernel == LVLIP_KERNEL_AUTO) {
-        // Measured on MI355X: the stream kernel leads on uniform
-        // MTU/jumbo segments, the flat sweep on mixed header/payload batches and
-        // stays within ~10 % elsewhere, so it is the choice when sizes are unknown.
+        // Measured on MI355X: the interleaved stream (k_window)
+        // leads on uniform MTU/jumbo segments, the flat sweep on mixed
+        // header/payload batches and stays within ~10 % elsewhere, so it is the
+        // choice when sizes are unknown.
         const int hint = cfg ? cfg->len_hint : 0;
         if (hint >= 512) {
             // the interleaved stream, shapes from scripts/shape_sweep.py
