@@ -535,8 +535,14 @@ def test_max_int_packet():
     assert want[1] == pyoracle.checksum(np.full(16, 0xFF, np.uint8), 0, (0x12345678 + (0xFFFF << 29)) & 0xFFFFFFFF)
     descs = dev_descs(d)
     for variant in [(lvlip.KERNEL_AUTO, 0, 0), (lvlip.KERNEL_WAVE, 2, 0), (lvlip.KERNEL_FLAT, 0, 0),
+                    (lvlip.KERNEL_FLAT, 4 | (2 << 8), 0), (lvlip.KERNEL_WINDOW, 2 | (3 << 8), 0),
+                    (lvlip.KERNEL_WINDOW, 3 | (1 << 8), 1), (lvlip.KERNEL_WFLAT, 0, 0),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0)]:
         assert list(run(base, descs, variant)) == list(want), variant
+    # AUTO with the caller's hint (the batch's average length: k_window, G 3)
+    out = lvlip.batch_torch(base, descs, None, len_hint=(n1 + (1 << 30)) // 2)
+    torch.cuda.synchronize()
+    assert list(out.cpu().numpy().view(np.uint16)) == list(want)
     del base, descs
     torch.cuda.empty_cache()
 
