@@ -31,6 +31,7 @@ extern "C" int lvlip_csum_batch_dev_ex(const void*, const lvlip_csum_desc*, uint
 namespace {
 
 constexpr size_t kDefaultArena = 64ull << 20;
+constexpr uint64_t kDirectMax = 4ull << 20;  // measured: DESIGN.md §5
 constexpr int kSlots = 2;
 
 inline uint64_t align16(uint64_t x) { return (x + 15ull) & ~15ull; }
@@ -39,6 +40,11 @@ struct Slot {
     uint8_t* h_bytes = nullptr;         // pinned
     lvlip_csum_desc* h_desc = nullptr;  // pinned
     uint16_t* h_out = nullptr;          // pinned
+    // the same three pinned buffers as device addresses (small pieces are read
+    // and written by the kernel in place, see launch_piece)
+    uint8_t* dh_bytes = nullptr;
+    lvlip_csum_desc* dh_desc = nullptr;
+    uint16_t* dh_out = nullptr;
     uint8_t* d_bytes = nullptr;
     lvlip_csum_desc* d_desc = nullptr;
     uint16_t* d_out = nullptr;
@@ -66,6 +72,7 @@ struct lvlip_csum_ctx {
     size_t arena = 0;     // bytes per slot
     uint32_t max_desc = 0;  // descriptors per slot
     int threads = 1;        // host threads for the gather into the pinned arena
+    uint64_t direct_max = 0;  // pieces up to this many bytes skip the copies
     Slot slot[kSlots];
     std::vector<Region> regions;
     char err[256] = "";
@@ -108,6 +115,23 @@ int drain(lvlip_csum_ctx* c, Slot& s) {
 int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uint16_t* user_out,
                  const uint8_t* src = nullptr, const uint8_t* dev_base = nullptr) {
     hipError_t e;
+    lvlip_launch_cfg cfg{};
+    cfg.kernel = LVLIP_KERNEL_AUTO;  // the piece's average length picks the kernel
+    cfg.len_hint = (int32_t)(bytes / count > 0x7fffffffull ? 0x7fffffff : bytes / count);
+    if (bytes <= c->direct_max && (dev_base || !src || src == s.h_bytes)) {
+        // A small piece: the copies' fixed costs (an SDMA round trip each way)
+        // outweigh moving the bytes, so the kernel reads the pinned arena (or
+        // the zero-copy region) and the descriptors over PCIe and writes the
+        // results straight into the pinned result buffer.
+        const int rc = lvlip_csum_batch_dev_ex(dev_base ? dev_base : s.dh_bytes, s.dh_desc, count,
+                                               s.dh_out, s.stream, &cfg);
+        if (rc != LVLIP_OK) return rc;
+        if ((e = hipEventRecord(s.done, s.stream)) != hipSuccess) return fail(c, e, "hipEventRecord");
+        s.user_out = user_out;
+        s.count = count;
+        s.busy = true;
+        return LVLIP_OK;
+    }
     if (!dev_base) {
         const uint64_t nb = src && src != s.h_bytes ? bytes : align16(bytes);
         if ((e = hipMemcpyAsync(s.d_bytes, src ? src : s.h_bytes, nb, hipMemcpyHostToDevice,
@@ -117,9 +141,6 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
     if ((e = hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)count * sizeof(lvlip_csum_desc),
                             hipMemcpyHostToDevice, s.stream)) != hipSuccess)
         return fail(c, e, "H2D descriptors");
-    lvlip_launch_cfg cfg{};
-    cfg.kernel = LVLIP_KERNEL_AUTO;  // the piece's average length picks the kernel
-    cfg.len_hint = (int32_t)(bytes / count > 0x7fffffffull ? 0x7fffffff : bytes / count);
     int rc = lvlip_csum_batch_dev_ex(dev_base ? dev_base : s.d_bytes, s.d_desc, count, s.d_out,
                                      s.stream, &cfg);
     if (rc != LVLIP_OK) return rc;
@@ -239,6 +260,13 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         int t = e ? atoi(e) : (int)(hw ? (hw < 8 ? hw : 8) : 1);
         c->threads = t < 1 ? 1 : (t > 64 ? 64 : t);
     }
+    // LVLIP_DIRECT_MAX: pieces of at most this many bytes skip the H2D/D2H
+    // copies (launch_piece); 0 turns that off
+    {
+        const char* e = getenv("LVLIP_DIRECT_MAX");
+        const long long v = e ? atoll(e) : (long long)kDirectMax;
+        c->direct_max = v > 0 ? (uint64_t)v : 0u;
+    }
     // descriptors per piece: one per 64 B of arena (a piece of smaller packets
     // simply ends at this count; the next piece takes the rest)
     c->max_desc = (uint32_t)(arena_bytes / 64 < 4096 ? 4096 : arena_bytes / 64);
@@ -255,7 +283,10 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
             (e = hipMalloc((void**)&s.d_desc, (size_t)c->max_desc * sizeof(lvlip_csum_desc))) != hipSuccess ||
             (e = hipMalloc((void**)&s.d_out, (size_t)c->max_desc * sizeof(uint16_t))) != hipSuccess ||
             (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
+            (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&s.dh_bytes, s.h_bytes, 0)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&s.dh_desc, s.h_desc, 0)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&s.dh_out, s.h_out, 0)) != hipSuccess) {
             fail(c, e, "lvlip_csum_ctx_create");
             for (auto& t : c->slot) free_slot(t);
             delete c;
