@@ -384,6 +384,29 @@ def test_host_flat_config_slices():
         assert np.array_equal(ctx.batch_host_flat(host, b.descs), want)
 
 
+@pytest.mark.parametrize("direct_max", ["0", "65536", "1000000000000"])
+def test_host_direct_and_copied_pieces(monkeypatch, direct_max):
+    """LVLIP_DIRECT_MAX (read when a context is made): pieces up to it are read
+    from the pinned arena by the kernel and answered into pinned memory; larger
+    ones go through the copy engine.  0 = always copies, 64 KiB = a mix within
+    one call, 1e12 = never copies.  Same bits either way."""
+    monkeypatch.setenv("LVLIP_DIRECT_MAX", direct_max)
+    b = workloads.make("mixed", n=20000)
+    host = b.host_bytes()
+    want = pyoracle.batch(host, b.descs, threads=THREADS)
+    with lvlip.Context(0, arena_bytes=192 << 10) as ctx:  # many pieces of ~192 KiB
+        assert np.array_equal(ctx.batch_host_flat(host, b.descs), want)
+        pk = [host[int(d["offset"]):int(d["offset"]) + max(int(d["len"]), 0)] for d in b.descs[:3000]]
+        st = [int(d["start_sum"]) for d in b.descs[:3000]]
+        assert np.array_equal(ctx.batch_host(pk, st), want[:3000])
+        assert np.array_equal(ctx.batch_host(pk[:7], st[:7]), want[:7])  # one tiny piece
+    buf = np.empty(b.nbytes + 64, dtype=np.uint8)[3:3 + b.nbytes]
+    buf[:] = host[:b.nbytes]
+    with lvlip.Context(0, arena_bytes=1 << 20) as ctx:
+        ctx.register(buf, lvlip.REG_ZEROCOPY)
+        assert np.array_equal(ctx.batch_host_flat(buf, b.descs), want)
+
+
 def test_lab_read_probe_sums():
     lab = lvlip.lab()
     a = torch.arange(0, 1 << 20, dtype=torch.int32, device="cuda")
