@@ -20,6 +20,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -32,6 +35,7 @@ namespace {
 
 constexpr size_t kDefaultArena = 64ull << 20;
 constexpr uint64_t kDirectMax = 4ull << 20;  // measured: DESIGN.md §5
+constexpr uint64_t kPieceMax = 32ull << 20;  // measured: DESIGN.md §5
 constexpr int kSlots = 2;
 
 inline uint64_t align16(uint64_t x) { return (x + 15ull) & ~15ull; }
@@ -65,6 +69,71 @@ struct Region {
     uint32_t flags = 0;
 };
 
+// The context's gather workers, started on first use and kept until the
+// context is destroyed, so that a piece of a few hundred KB can be gathered
+// by several threads (a std::thread start costs more than copying 1 MB).
+// Only the context's owning thread submits work.
+class GatherPool {
+   public:
+    ~GatherPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_job_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    // fn(0 .. parts-1), part 0 on the calling thread; returns when all are done
+    void run(int parts, const std::function<void(int)>& fn) {
+        if (parts <= 1) {
+            fn(0);
+            return;
+        }
+        while ((int)th_.size() < parts - 1) {
+            // a new worker waits for the generation after the current one (this
+            // thread is gen_'s only writer, so it may read it unlocked)
+            const int id = (int)th_.size() + 1;
+            const uint64_t g0 = gen_;
+            th_.emplace_back([this, id, g0] { worker(id, g0); });
+        }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &fn;
+            parts_ = parts;
+            pending_ = parts - 1;
+            ++gen_;
+        }
+        cv_job_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> g(m_);
+        cv_done_.wait(g, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+   private:
+    void worker(int id, uint64_t seen) {
+        std::unique_lock<std::mutex> g(m_);
+        for (;;) {
+            cv_job_.wait(g, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            if (id >= parts_) continue;
+            const std::function<void(int)>* job = job_;
+            g.unlock();
+            (*job)(id);
+            g.lock();
+            if (--pending_ == 0) cv_done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_job_, cv_done_;
+    const std::function<void(int)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    int parts_ = 0, pending_ = 0;
+    bool stop_ = false;
+};
+
 }  // namespace
 
 struct lvlip_csum_ctx {
@@ -73,8 +142,10 @@ struct lvlip_csum_ctx {
     uint32_t max_desc = 0;  // descriptors per slot
     int threads = 1;        // host threads for the gather into the pinned arena
     uint64_t direct_max = 0;  // pieces up to this many bytes skip the copies
+    uint64_t piece = 0;       // bytes per piece (<= arena; a larger packet gets its own)
     Slot slot[kSlots];
     std::vector<Region> regions;
+    GatherPool pool;
     char err[256] = "";
 };
 
@@ -179,23 +250,19 @@ struct DeviceGuard {
     }
 };
 
-// Run fn(lo, hi) over [0, n) split into `threads` contiguous ranges.  The
-// gather into pinned memory is host-memory-bandwidth bound: one core moves
-// ~25-30 GB/s, below PCIe Gen5 x16, so large pieces are copied by several.
+// Run fn(lo, hi) over [0, n) split into up to c->threads contiguous ranges of
+// at least min_per_thread.  The gather into pinned memory is host-memory-
+// bandwidth bound: one core moves ~25-30 GB/s, below PCIe Gen5 x16, so a piece
+// is copied by several of the context's pool threads.
 template <class F>
-void parallel_ranges(int threads, uint64_t n, uint64_t min_per_thread, F fn) {
-    uint64_t t = threads > 1 ? (uint64_t)threads : 1u;
+void parallel_ranges(lvlip_csum_ctx* c, uint64_t n, uint64_t min_per_thread, F fn) {
+    uint64_t t = c->threads > 1 ? (uint64_t)c->threads : 1u;
     if (n / min_per_thread < t) t = n / min_per_thread ? n / min_per_thread : 1u;
     if (t <= 1) {
         fn(0, n);
         return;
     }
-    std::vector<std::thread> pool;
-    pool.reserve(t - 1);
-    for (uint64_t k = 1; k < t; ++k)
-        pool.emplace_back([=] { fn(n * k / t, n * (k + 1) / t); });
-    fn(0, n / t);
-    for (auto& th : pool) th.join();
+    c->pool.run((int)t, [&](int k) { fn(n * (uint64_t)k / t, n * (uint64_t)(k + 1) / t); });
 }
 
 // The registered region holding [p, p + len), or nullptr.
@@ -266,6 +333,14 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         const char* e = getenv("LVLIP_DIRECT_MAX");
         const long long v = e ? atoll(e) : (long long)kDirectMax;
         c->direct_max = v > 0 ? (uint64_t)v : 0u;
+    }
+    // LVLIP_PIECE_MAX: bytes per piece, so that even a batch of a few MB is cut
+    // into pieces whose gather, copies and kernel overlap across the two slots
+    {
+        const char* e = getenv("LVLIP_PIECE_MAX");
+        const long long v = e ? atoll(e) : (long long)kPieceMax;
+        const uint64_t pm = v > 0 ? align16((uint64_t)v) : arena_bytes;
+        c->piece = pm < arena_bytes ? pm : arena_bytes;
     }
     // descriptors per piece: one per 64 B of arena (a piece of smaller packets
     // simply ends at this count; the next piece takes the rest)
@@ -392,7 +467,7 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
         while (i < n && k < c->max_desc) {
             const int32_t len = pkts[i].len;
             const uint64_t need = len > 0 ? (uint64_t)len : 0;
-            if (off + need > c->arena) break;
+            if (off + need > (k ? c->piece : c->arena)) break;
             s.h_desc[k].offset = off;
             s.h_desc[k].len = len;
             s.h_desc[k].start_sum = pkts[i].start_sum;
@@ -405,7 +480,7 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
             uint8_t* dst = s.h_bytes;
             const lvlip_csum_desc* hd = s.h_desc;
             const lvlip_csum_iov* src = pkts + first;
-            parallel_ranges(c->threads, k, 4096, [=](uint64_t lo, uint64_t hi) {
+            parallel_ranges(c, k, 1024, [=](uint64_t lo, uint64_t hi) {
                 for (uint64_t q = lo; q < hi; ++q)
                     if (hd[q].len > 0) memcpy(dst + hd[q].offset, src[q].ptr, (size_t)hd[q].len);
             });
@@ -452,7 +527,8 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
             const uint64_t e = o + (d[i].len > 0 ? (uint64_t)d[i].len : 0);
             const uint64_t nlo = (o & ~15ull) < lo16 ? (o & ~15ull) : lo16;
             const uint64_t nhi = e > hi ? e : hi;
-            if (align16(nhi) - nlo > c->arena) break;  // k >= 1: single spans fit (checked above)
+            // k >= 1 here: a single span always fits the arena (checked above)
+            if (align16(nhi) - nlo > (k ? c->piece : c->arena)) break;
             lo16 = nlo;
             hi = nhi;
             ++k;
@@ -468,7 +544,7 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
         } else if (span) {
             uint8_t* dst = s.h_bytes;
             const uint8_t* src = b + lo16;
-            parallel_ranges(c->threads, span, 4u << 20, [=](uint64_t lo, uint64_t hi) {
+            parallel_ranges(c, span, 512u << 10, [=](uint64_t lo, uint64_t hi) {
                 memcpy(dst + lo, src + lo, hi - lo);
             });
         }
