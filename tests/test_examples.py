@@ -1,0 +1,40 @@
+"""examples/tx_rx_batch.c: INTEGRATION.md's TX/RX sketches as a plain C program
+on the C ABI alone (built by __graft_entry__.build() / `make -C examples`).
+
+On the GPU it fills the TCP and IPv4 checksums of 65 536 level-ip frames in one
+call and checks every field against the per-call drop-in (tcp_v4_checksum's and
+ip_send_check's arithmetic, src/tcp.c:87-103, src/ip_output.c:8-12), then
+checks ip_rcv's verdicts for the same frames with every 97th one corrupted.
+Without a GPU it must fail loudly: there is no CPU fallback behind the batch
+calls."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "examples", "build", "tx_rx_batch")
+
+
+def _exe():
+    if not os.path.exists(EXE):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "examples")], check=True,
+                       capture_output=True)
+    return EXE
+
+
+def test_example_fails_loudly_without_gpu():
+    import lvlip
+
+    if lvlip.device_count() > 0:
+        pytest.skip("a GPU is present")
+    r = subprocess.run([_exe(), "64"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "no HIP device" in r.stderr, (r.returncode, r.stderr)
+
+
+@pytest.mark.gpu
+def test_example_tx_rx_batch():
+    assert os.path.exists(EXE), "examples/build/tx_rx_batch not built (run __graft_entry__.build())"
+    r = subprocess.run([EXE, "65536"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "tx_rx_batch ok: 65536 frames" in r.stdout, r.stdout
