@@ -311,10 +311,10 @@ def main():
     achieved = b.algo_bytes / (kern_ms / 1e3) / 1e9  # rank 0's kernel, algorithmic bytes
     kernel_label = f"{args.kernel}-u{args.unroll}-w{args.waves_per_cu}"
     # AUTO's choice (dispatch_one in csum_kernels.hip): the interleaved stream
-    # from 512 B, the flat sweep below
+    # from 896 B, the flat sweep below
     chosen = args.kernel
     if kernel == lvlip.KERNEL_AUTO:
-        chosen = "window" if len_hint >= 512 else "flat"
+        chosen = "window" if len_hint >= 896 else "flat"
 
     diag = {"settle": {"launches": settle_n, "ms": round(settle_ms, 1)}}
     if scatter_diag is not None:

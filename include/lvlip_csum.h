@@ -120,7 +120,7 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
                          uint32_t n, uint16_t *out, void *stream);
 
 /* Kernel selection for lvlip_csum_batch_dev_ex.  AUTO picks by len_hint:
- * >= 512 B -> WINDOW (shape by the hint); otherwise or unknown ->
+ * >= 896 B -> WINDOW (shape by the hint); otherwise or unknown ->
  * FLAT (measured: DESIGN.md §5). */
 #define LVLIP_KERNEL_AUTO        0  /* the default                                 */
 #define LVLIP_KERNEL_WAVE        1  /* one wavefront per packet, persistent stream,

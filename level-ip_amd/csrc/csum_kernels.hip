@@ -22,12 +22,12 @@
 //
 // Kernels (roofline: HBM read bandwidth; ~1 VALU op per loaded dword, no MFMA;
 // DESIGN.md §4):
-//   k_window  : the default from 512 B.  One wavefront per packet, persistent, a
+//   k_window  : the default from 896 B.  One wavefront per packet, persistent, a
 //               ring of 2-KiB pieces in flight per wave; packets dealt to the
 //               waves in small groups round robin over the grid, so the waves in
 //               flight read one narrow window of the batch.
 //   k_stream  : the same ring with contiguous per-wave ranges (A/B).
-//   k_flat2   : the default below 512 B (ragged batches: 20-B headers next to
+//   k_flat2   : the default below 896 B (ragged batches: 20-B headers next to
 //               payloads).  A chunk-balanced tile sweep over 16-B chunks that
 //               crosses packet boundaries; segment sums by a DPP prefix scan.
 //               Also the frame calls' kernel (flat_src.h, skb_dev.hip).
@@ -1467,7 +1467,7 @@ int window_group(int requested, int len_hint) {
     if (v == 1 || v == 2 || v == 3 || v == 4 || v == 8) return v;
     // no group in the request: as AUTO (dispatch_one) picks for this hint
     if (len_hint >= 4096) return 3;
-    if (len_hint >= 2048) return 2;
+    if (len_hint >= 1792) return 2;
     return 4;
 }
 
@@ -1559,17 +1559,21 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         // header/payload batches and stays within ~10 % elsewhere, so it is the
         // choice when sizes are unknown.
         const int hint = cfg ? cfg->len_hint : 0;
-        if (hint >= 512) {
+        if (hint >= 896) {
             // the interleaved stream, shapes from scripts/shape_sweep.py
             // (DESIGN.md §4): 2 pieces in flight per wave; more waves per CU for
-            // smaller packets (per-packet work); groups of 4 packets up to 2 KiB,
-            // 2 up to 4 KiB, 3 for jumbo packets (power-of-two group bytes such as
-            // 2 x 4096 measured 3 % slow)
+            // smaller packets (per-packet work); groups of 4 packets below
+            // 1792 B, 2 up to 4 KiB, 3 for jumbo packets (power-of-two group
+            // bytes such as 2 x 4096 measured 3 % slow)
             kernel = LVLIP_KERNEL_WINDOW;
-            if (wpc <= 0) wpc = hint < 1280 ? 16 : (hint < 2048 ? 12 : 8);
-            if (unroll <= 0) unroll = 2 | ((hint < 2048 ? 4 : (hint < 4096 ? 2 : 3)) << 8);
+            if (wpc <= 0) wpc = hint < 1280 ? 16 : (hint < 1792 ? 12 : 8);
+            if (unroll <= 0) unroll = 2 | ((hint < 1792 ? 4 : (hint < 4096 ? 2 : 3)) << 8);
         } else {
+            // below ~900 B the flat sweep leads (uniform 512 / 768 B: 6 442 /
+            // 6 482 vs 3 973 / 5 916 GB/s for the stream), 4 loads per round
+            // below 320 B (64 / 128 B: 4 973 / 6 114 vs 3 825 / 5 448 with 8)
             kernel = LVLIP_KERNEL_FLAT;
+            if (unroll <= 0 && hint > 0 && hint < 320) unroll = 4;
         }
     }
 

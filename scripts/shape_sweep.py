@@ -8,7 +8,8 @@ dispatch_one (csum_kernels.hip).
 env: SH_LENS (default 512,768,1024,1500,2048,3000,4096,9000),
      SH_SHAPES (default 2x8,2x16,3x8,3x12,4x8,4x16), SH_ROUNDS (2),
      SH_WINDOW (k_window shapes RxWxG: pieces in flight, waves/CU, packets per group),
-     SH_TOTAL (bytes of packet slots per length, default 1.5e9)
+     SH_TOTAL (bytes of packet slots per length, default 1.5e9),
+     SH_FLAT (k_flat2 unrolls, e.g. 8,4; default none)
 writes JSON to argv[1]."""
 import json
 import os
@@ -38,7 +39,7 @@ def main():
     out_path = sys.argv[1] if len(sys.argv) > 1 else None
     lens = [int(x) for x in os.environ.get("SH_LENS", "512,768,1024,1500,2048,3000,4096,9000").split(",")]
     shapes = [tuple(int(v) for v in s.split("x"))
-              for s in os.environ.get("SH_SHAPES", "2x8,2x16,3x8,3x12,4x8,4x16").split(",")]
+              for s in os.environ.get("SH_SHAPES", "2x8,2x16,3x8,3x12,4x8,4x16").split(",") if s]
     rounds = int(os.environ.get("SH_ROUNDS", "2"))
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream(dev)
@@ -63,6 +64,8 @@ def main():
         for sh in filter(None, os.environ.get("SH_WINDOW", "").split(",")):
             r, w, gsz = (int(v) for v in sh.split("x"))
             variants.append(("window", r | (gsz << 8), w))
+        for u in filter(None, os.environ.get("SH_FLAT", "").split(",")):
+            variants.append(("flat", int(u), 0))
         for _ in range(rounds):
             for k, r, w in variants:
                 def f():
