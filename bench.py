@@ -377,16 +377,17 @@ def timed(torch, fn, stream, reps=20, warm=3):
 
 def sweep(lvlip, torch, base, descs, out, b, stream):
     res = {}
-    variants = [("wave", 2, 8), ("wave", 2, 12), ("wave", 2, 16), ("wave", 3, 12), ("wave", 3, 16),
-                ("wave", 4, 16), ("wave_simple", 2, 0), ("wave_lds", 2, 0), ("flat", 2, 0),
-                ("flat", 4, 0), ("flat", 8, 0), ("flat_v1", 0, 0)]
+    variants = [("window", 2 | (4 << 8), 16), ("window", 2 | (4 << 8), 12), ("window", 2 | (2 << 8), 8),
+                ("window", 2 | (3 << 8), 8), ("wave", 2, 8), ("wave", 2, 12), ("wave", 3, 12),
+                ("wave_simple", 2, 0), ("wave_lds", 2, 0), ("flat", 4, 0), ("flat", 8, 0),
+                ("flat", 8 | (2 << 8), 0), ("wflat", 0, 0), ("flat_v1", 0, 0)]
     for rnd in range(2):  # interleaved rounds in one process
         for k, u, w in variants:
             def f():
                 lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
                                 stream.cuda_stream, lvlip.KERNEL_NAMES[k], u, w)
             ms = timed(torch, f, stream, reps=10)
-            key = f"{k}-u{u}-w{w}"
+            key = f"{k}-u{u:#x}-w{w}"
             res.setdefault(key, []).append(round(b.algo_bytes / ms / 1e6, 1))
     for k, v in res.items():
         log(f"sweep {k:18s} GB/s {v}")
