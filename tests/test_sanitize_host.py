@@ -4,8 +4,10 @@ runner greps ThreadSanitizer reports, tests/test-run-all:41).
 
 tests/sanitize/host_san.c drives level-ip_amd/csrc/csum_cpu.c (the per-call
 drop-in, AVX-512, AVX2 and portable paths) and level-ip_amd/csrc/skb_batch.c (the frame
-calls' multi-threaded host steps) against the oracle; see its header.  Host
-code only: GPU sanitizers are not available on the MI355X pool."""
+calls' multi-threaded host steps) against the oracle; see its header.
+tests/sanitize/pool_san.cpp drives the host context's gather pool
+(level-ip_amd/csrc/gather_pool.h) on its own.  Host code only: GPU sanitizers
+are not available on the MI355X pool."""
 import os
 import shutil
 import subprocess
@@ -62,4 +64,27 @@ def test_host_code_tsan(tmp_path):
             pytest.skip("TSan needs ASLR off and setarch is absent")
         r = subprocess.run([setarch, os.uname().machine, "-R", exe],
                            capture_output=True, text=True, timeout=600)
+    _check(r)
+
+
+@pytest.mark.parametrize("kind", ["tsan", "asan"])
+def test_gather_pool(tmp_path, kind):
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / f"pool_{kind}")
+    r = subprocess.run([cxx, "-std=c++17", "-O1", "-g", "-pthread",
+                        "-I", os.path.join(ROOT, "level-ip_amd", "csrc"), *FLAGS[kind],
+                        os.path.join(ROOT, "tests", "sanitize", "pool_san.cpp"), "-o", exe],
+                       capture_output=True, text=True)
+    if r.returncode != 0 and "cannot find" in r.stderr:
+        pytest.skip(f"{kind} runtime not installed: {r.stderr.strip()[:200]}")
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    if kind == "tsan" and r.returncode != 0 and "unexpected memory mapping" in r.stderr:
+        setarch = shutil.which("setarch")
+        if setarch is None:
+            pytest.skip("TSan needs ASLR off and setarch is absent")
+        r = subprocess.run([setarch, os.uname().machine, "-R", exe], capture_output=True, text=True,
+                           timeout=300)
     _check(r)
