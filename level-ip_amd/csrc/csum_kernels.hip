@@ -815,6 +815,34 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp 
     return before + incl - v;
 }
 
+// two exclusive prefixes over the 256 threads for one barrier pair; *ta, *tb
+// get the totals
+__device__ __forceinline__ void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* s_tmp /* >= 8 */,
+                                                 uint32_t* ea, uint32_t* eb, uint32_t* ta,
+                                                 uint32_t* tb) {
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    const uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+    if (lane == 63u) {
+        s_tmp[wid] = ia;
+        s_tmp[4u + wid] = ib;
+    }
+    __syncthreads();
+    uint32_t ba = 0, bb = 0, aa = 0, ab = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t x = s_tmp[k], y = s_tmp[4u + k];
+        ba += (k < wid) ? x : 0u;
+        bb += (k < wid) ? y : 0u;
+        aa += x;
+        ab += y;
+    }
+    __syncthreads();
+    *ea = ba + ia - a;
+    *eb = bb + ib - b;
+    *ta = aa;
+    *tb = ab;
+}
+
 // byte mask of bytes [b0, b1) of a 16-B chunk that fall in dword j
 __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
     const int s = min(max(b0 - 4 * j, 0), 4);
@@ -867,13 +895,13 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
     }
     s_acc[t] = 0u;
     for (uint32_t g = t; g < FGROUPS; g += FT) s_grp[g] = make_uint2(0u, 0u);
-    uint32_t nbig = 0;
-    const uint32_t big_pos = block_excl_scan(big ? 1u : 0u, s_tmp, &nbig);
+    // one scan pass for three prefixes: big packets (high half) and swept
+    // packets (low half, both <= 256) packed in one word, chunks in the other
+    uint32_t e1 = 0, cstart = 0, t1 = 0, C = 0;
+    block_excl_scan2((big ? 0x10000u : 0u) | (nch ? 1u : 0u), nch, s_tmp, &e1, &cstart, &t1, &C);
+    const uint32_t big_pos = e1 >> 16, nbig = t1 >> 16;
+    const uint32_t rank = e1 & 0xffffu;
     if (big) s_big[big_pos] = t;
-    uint32_t nsmall = 0;
-    const uint32_t rank = block_excl_scan(nch ? 1u : 0u, s_tmp, &nsmall);
-    uint32_t C = 0;
-    const uint32_t cstart = block_excl_scan(nch, s_tmp, &C);
     if (nch) {
         s_rec[rank] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), cstart, meta);
         const uint32_t g = cstart >> 6, b = cstart & 63u;
