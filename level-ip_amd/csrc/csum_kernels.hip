@@ -796,25 +796,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-// exclusive prefix over the 256 threads of a workgroup; *total gets the sum
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp /* >= 4 */,
-                                                    uint32_t* total) {
-    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-    const uint32_t incl = wave_incl_scan(v);
-    if (lane == 63u) s_tmp[wid] = incl;
-    __syncthreads();
-    uint32_t before = 0, all = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t t = s_tmp[k];
-        before += (k < wid) ? t : 0u;
-        all += t;
-    }
-    __syncthreads();
-    *total = all;
-    return before + incl - v;
-}
-
 // two exclusive prefixes over the 256 threads for one barrier pair; *ta, *tb
 // get the totals
 __device__ __forceinline__ void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* s_tmp /* >= 8 */,
@@ -901,25 +882,21 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
     block_excl_scan2((big ? 0x10000u : 0u) | (nch ? 1u : 0u), nch, s_tmp, &e1, &cstart, &t1, &C);
     const uint32_t big_pos = e1 >> 16, nbig = t1 >> 16;
     const uint32_t rank = e1 & 0xffffu;
+    const uint32_t G = (C + 63u) >> 6;
     if (big) s_big[big_pos] = t;
     if (nch) {
         s_rec[rank] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), cstart, meta);
         const uint32_t g = cstart >> 6, b = cstart & 63u;
         if (b < 32u) atomicOr(&s_grp[g].x, 1u << b);
         else atomicOr(&s_grp[g].y, 1u << (b - 32u));
+        // heads before group g = swept packets that start before chunk 64 g.
+        // The packets' chunk ranges tile [0, C) in rank order, so for every
+        // group that starts inside (cstart, cstart + nch] that count is this
+        // packet's rank + 1 (at most 3 groups: nch <= FCAP = 128)
+        for (uint32_t gg = g + 1u; gg < G && (gg << 6) <= cstart + nch; ++gg)
+            s_hb[gg] = (uint16_t)(rank + 1u);
     }
-    __syncthreads();
-    const uint32_t G = (C + 63u) >> 6;
-    // heads before each group: two groups per thread, block scan of the popcounts
-    {
-        const uint32_t g0 = 2u * t, g1 = 2u * t + 1u;
-        const uint32_t p0 = g0 < G ? (uint32_t)__popcll(((uint64_t)s_grp[g0].y << 32) | s_grp[g0].x) : 0u;
-        const uint32_t p1 = g1 < G ? (uint32_t)__popcll(((uint64_t)s_grp[g1].y << 32) | s_grp[g1].x) : 0u;
-        uint32_t tot = 0;
-        const uint32_t before = block_excl_scan(p0 + p1, s_tmp, &tot);
-        if (g0 < G) s_hb[g0] = (uint16_t)before;
-        if (g1 < G) s_hb[g1] = (uint16_t)(before + p0);
-    }
+    if (t == 0u) s_hb[0] = 0;
     __syncthreads();
 
     // ---- phase 2: sweep the chunk space, groups wid, wid+4, ... ; U per round.
