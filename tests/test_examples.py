@@ -38,3 +38,22 @@ def test_example_tx_rx_batch():
     r = subprocess.run([EXE, "65536"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "tx_rx_batch ok: 65536 frames" in r.stdout, r.stdout
+
+
+def test_install_and_build_against_it(tmp_path):
+    """`make -C level-ip_amd install PREFIX=...` gives a level-ip build what it
+    links: the example compiles and links against the
+    installed headers and library alone."""
+    prefix = tmp_path / "prefix"
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "level-ip_amd"), "install",
+                    f"PREFIX={prefix}"], check=True, capture_output=True)
+    for f in ("include/lvlip_csum.h", "include/lvlip_skb.h", "lib/liblvlip_csum.so"):
+        assert (prefix / f).exists(), f
+    exe = tmp_path / "tx_rx_batch"
+    r = subprocess.run(["gcc", "-std=c99", "-D_POSIX_C_SOURCE=199309L", "-O2", "-Wall", "-Werror",
+                        "-I", str(prefix / "include"), os.path.join(ROOT, "examples", "tx_rx_batch.c"),
+                        "-L", str(prefix / "lib"), "-llvlip_csum", f"-Wl,-rpath,{prefix / 'lib'}",
+                        "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run(["ldd", str(exe)], capture_output=True, text=True)
+    assert str(prefix / "lib" / "liblvlip_csum.so") in r.stdout, r.stdout
