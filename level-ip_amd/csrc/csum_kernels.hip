@@ -1576,9 +1576,10 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         } else {
             // below ~900 B the flat sweep leads (uniform 512 / 768 B: 6 442 /
             // 6 482 vs 3 973 / 5 916 GB/s for the stream), 4 loads per round
-            // below 320 B (64 / 128 B: 4 973 / 6 114 vs 3 825 / 5 448 with 8)
+            // below 320 B (64 / 128 B: 4 973 / 6 114 vs 3 825 / 5 448 with 8),
+            // 2 below 40 B (IPv4 headers alone, 20 B: 2 356 vs 2 251 with 4)
             kernel = LVLIP_KERNEL_FLAT;
-            if (unroll <= 0 && hint > 0 && hint < 320) unroll = 4;
+            if (unroll <= 0 && hint > 0 && hint < 320) unroll = hint < 40 ? 2 : 4;
         }
     }
 

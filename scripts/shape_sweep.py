@@ -9,7 +9,8 @@ env: SH_LENS (default 512,768,1024,1500,2048,3000,4096,9000),
      SH_SHAPES (default 2x8,2x16,3x8,3x12,4x8,4x16), SH_ROUNDS (2),
      SH_WINDOW (k_window shapes RxWxG: pieces in flight, waves/CU, packets per group),
      SH_TOTAL (bytes of packet slots per length, default 1.5e9),
-     SH_FLAT (k_flat2 unrolls, e.g. 8,4; default none)
+     SH_FLAT (k_flat2 unrolls, e.g. 8,4; default none),
+     SH_WFLAT (k_wflat shapes UxWxD: loads per round, waves/CU, descriptors per tile)
 writes JSON to argv[1]."""
 import json
 import os
@@ -66,13 +67,16 @@ def main():
             variants.append(("window", r | (gsz << 8), w))
         for u in filter(None, os.environ.get("SH_FLAT", "").split(",")):
             variants.append(("flat", int(u), 0))
+        for sh in filter(None, os.environ.get("SH_WFLAT", "").split(",")):
+            u, w, dd = (int(v) for v in sh.split("x"))
+            variants.append(("wflat", u | (dd << 8), w))
         for _ in range(rounds):
             for k, r, w in variants:
                 def f():
                     lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), n, out.data_ptr(), s.cuda_stream,
                                     lvlip.KERNEL_NAMES[k], r, w, L)
                 ms = timed(f, s)
-                key = f"{k}-{r & 0xff}x{w}" + (f"g{r >> 8}" if r >> 8 else "")
+                key = f"{k}-{r & 0xff}x{w}" + (f"g{r >> 8}" if r >> 8 else "")  # g = group / tile
                 row.setdefault(key, []).append(round(algo / ms / 1e6, 1))
         best = max(row, key=lambda k: max(row[k]))
         print(f"L={L:5d} n={n:8d} " + "  ".join(f"{k}:{max(v):7.1f}" for k, v in row.items()) + f"  best {best}",
