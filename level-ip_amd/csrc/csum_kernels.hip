@@ -1572,7 +1572,17 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             // bytes such as 2 x 4096 measured 3 % slow)
             kernel = LVLIP_KERNEL_WINDOW;
             if (wpc <= 0) wpc = hint < 1280 ? 16 : (hint < 1792 ? 12 : 8);
-            if (unroll <= 0) unroll = 2 | ((hint < 1792 ? 4 : (hint < 4096 ? 2 : 3)) << 8);
+            if (unroll <= 0) {
+                // ... but at least 16 groups per wave, or the last round of
+                // groups leaves most waves idle (45 776 packets of 64 KiB: G 3
+                // 6 698, G 1 6 974 GB/s)
+                int dev = 0;
+                (void)hipGetDevice(&dev);
+                const uint64_t nw = (uint64_t)cu_count(dev) * (uint64_t)wpc;
+                int g = hint < 1792 ? 4 : (hint < 4096 ? 2 : 3);
+                while (g > 1 && (uint64_t)n < 16ull * (uint64_t)g * nw) --g;
+                unroll = 2 | (g << 8);
+            }
         } else {
             // below ~900 B the flat sweep leads (uniform 512 / 768 B: 6 442 /
             // 6 482 vs 3 973 / 5 916 GB/s for the stream), 4 loads per round
