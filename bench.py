@@ -63,7 +63,8 @@ def parse():
                    help="packets (frames for mixed) per rank (--packets under torch.distributed.run, "
                         "whose own parser takes --n for a prefix of its options)")
     p.add_argument("--kernel", default="auto",
-                   choices=["auto", "wave", "wave_lds", "flat", "wave_simple", "flat_v1", "window", "wflat"])
+                   choices=["auto", "wave", "wave_lds", "flat", "wave_simple", "flat_v1", "window", "wflat",
+                            "lane"])
     p.add_argument("--unroll", type=int, default=0)
     p.add_argument("--waves-per-cu", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -84,7 +85,8 @@ def log(*a):
 
 
 # the device function each --kernel choice runs (what the PMC records name)
-KERNEL_FN = {"window": "k_window", "wave": "k_stream", "flat": "k_flat2", "wflat": "k_wflat"}
+KERNEL_FN = {"window": "k_window", "wave": "k_stream", "flat": "k_flat2", "wflat": "k_wflat",
+             "lane": "k_lane"}
 
 
 def traffic_from_profiles(workload: str, kernel_label: str, kernel_fn: str):
@@ -311,10 +313,10 @@ def main():
     achieved = b.algo_bytes / (kern_ms / 1e3) / 1e9  # rank 0's kernel, algorithmic bytes
     kernel_label = f"{args.kernel}-u{args.unroll}-w{args.waves_per_cu}"
     # AUTO's choice (dispatch_one in csum_kernels.hip): the interleaved stream
-    # from 896 B, the flat sweep below
+    # from 896 B, lane groups up to 32 B, the flat sweep between
     chosen = args.kernel
     if kernel == lvlip.KERNEL_AUTO:
-        chosen = "window" if len_hint >= 896 else "flat"
+        chosen = "window" if len_hint >= 896 else ("lane" if 0 < len_hint <= 32 else "flat")
 
     diag = {"settle": {"launches": settle_n, "ms": round(settle_ms, 1)}}
     if scatter_diag is not None:

@@ -120,8 +120,8 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
                          uint32_t n, uint16_t *out, void *stream);
 
 /* Kernel selection for lvlip_csum_batch_dev_ex.  AUTO picks by len_hint:
- * >= 896 B -> WINDOW (shape by the hint); otherwise or unknown ->
- * FLAT (measured: DESIGN.md §5). */
+ * >= 896 B -> WINDOW (shape by the hint); 1-32 B -> LANE; otherwise or
+ * unknown -> FLAT (measured: DESIGN.md §4-5). */
 #define LVLIP_KERNEL_AUTO        0  /* the default                                 */
 #define LVLIP_KERNEL_WAVE        1  /* one wavefront per packet, persistent stream,
                                        contiguous ranges per wave (A/B)        */
@@ -136,6 +136,8 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
                                        window of the batch in flight)          */
 #define LVLIP_KERNEL_WFLAT       9  /* FLAT's chunk sweep, one wave per tile of
                                        descriptors, tiles dealt round robin    */
+#define LVLIP_KERNEL_LANE       10  /* a few lanes per packet, chunks summed in
+                                       registers (batches of small packets)   */
 
 typedef struct lvlip_launch_cfg {
     int32_t  kernel;        /* LVLIP_KERNEL_*                               */
@@ -147,7 +149,11 @@ typedef struct lvlip_launch_cfg {
                                per tile << 8 (16, 32 or 64; 0 = 32);
                                FLAT: 64-chunk loads per round | group order
                                << 8 (1 interleaved, 2 quarters, 3 blocks;
-                               0 = LVLIP_FLAT_GROUPS, else quarters)         */
+                               0 = LVLIP_FLAT_GROUPS, else quarters);
+                               LANE: packets per lane group | 16-B chunks
+                               per lane << 8 | lanes per packet << 16 (1, 2,
+                               4, 8); longer packets go to a whole-wave
+                               loop (0 = 4 | 2 << 8 | 2 << 16)              */
     int32_t  waves_per_cu;  /* WAVE: resident waves per CU (0 = 8); others:
                                grid cap (0 = one wave per packet)           */
     int32_t  len_hint;      /* average packet length in bytes if the caller

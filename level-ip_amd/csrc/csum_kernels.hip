@@ -1314,6 +1314,109 @@ __global__ __launch_bounds__(256) void k_wflat(const uint8_t* __restrict__ base,
     }
     if (st_prev) out[i_prev] = res_prev;
 }
+
+// ------------------------------------------------ k_lane (small packets) --
+//
+// S lanes per packet (S = 1, 2, 4 or 8), for batches of packets a few 16-B
+// chunks long (20-B IPv4 headers alone, 40-64-B headers and echo payloads).
+// The flat sweep's per-tile plan (three block scans, the head bitmaps, the
+// records, two LDS round trips per group) costs about as much as sweeping a
+// tile of such packets: a 256-descriptor tile of 20-B headers is 8 KB of
+// bytes.  Here a group of S lanes reads its packet's descriptor (every lane
+// of the group the same one: one coalesced wave load per P), then lane s of
+// the group reads the packet's aligned chunks s, s + S, ..., up to K of them,
+// straight from the packet's address, and sums them in registers; an xor
+// butterfly over the group adds the S partial sums.  No LDS and no barrier.
+// With S chunks per packet slot (20-B headers in 32-B slots: S = 2) one wave
+// load covers 64 consecutive chunks, so every load instruction is one
+// contiguous 1-KiB read; with S = 1 the lanes of one load are a slot apart
+// and a load touches 64 slots' lines (measured: 64-B packets 2.6 TB/s at
+// S = 1).  Bytes outside the packet (the first chunk's lead-in, the last
+// chunk's tail) are masked in the lane; odd-address packets are byte-swapped
+// within u16 halves (see the file header).  A packet longer than S x K
+// chunks is summed by the whole wave after the group phase
+// (wave_packet_sum), one packet at a time.
+template <int S, int P, int K>
+__global__ __launch_bounds__(256) void k_lane(const uint8_t* __restrict__ base,
+                                              const lvlip_csum_desc* __restrict__ descs,
+                                              uint32_t n, uint16_t* __restrict__ out) {
+    static_assert(S == 1 || S == 2 || S == 4 || S == 8, "lanes per packet");
+    constexpr uint32_t PB = 256 / S;  // packets per block and p
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t sub = threadIdx.x & (uint32_t)(S - 1);
+    const uint32_t i0 = blockIdx.x * (PB * (uint32_t)P) + threadIdx.x / (uint32_t)S;
+    uint4 dd[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const uint32_t i = i0 + PB * p;
+        dd[p] = i < n ? load_global(reinterpret_cast<uint64_t>(descs + i)) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    uint64_t a0[P];
+    uint32_t lo[P], nch[P], lastv[P];
+    uint4 x[P][K];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const uint64_t abs = reinterpret_cast<uint64_t>(base) + (((uint64_t)dd[p].y << 32) | dd[p].x);
+        const int32_t len = (int32_t)dd[p].z;
+        a0[p] = abs & ~15ull;
+        lo[p] = (uint32_t)(abs & 15ull);
+        const uint64_t span = (uint64_t)lo[p] + (uint64_t)(uint32_t)(len > 0 ? len : 0);
+        nch[p] = len > 0 ? (uint32_t)((span + 15u) >> 4) : 0u;
+        lastv[p] = len > 0 ? (uint32_t)(span - 16ull * (nch[p] - 1u)) : 16u;
+        const bool in_group = nch[p] <= (uint32_t)(S * K);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = sub + (uint32_t)(S * k);
+            x[p][k] = (in_group && c < nch[p]) ? load_nt_global(a0[p] + 16ull * c)
+                                               : make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    uint32_t acc[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const uint32_t sel = (lo[p] & 1u) ? 0x02030001u : 0x03020100u;
+        uint32_t a = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = sub + (uint32_t)(S * k);
+            uint4 v = x[p][k];
+            const int b0 = c == 0u ? (int)lo[p] : 0;
+            const int b1 = c + 1u == nch[p] ? (int)lastv[p] : 16;
+            if (c == 0u || c + 1u == nch[p]) v = mask_chunk(v, b0, b1);
+            a = dot2_acc(__builtin_amdgcn_perm(v.x, v.x, sel), a);
+            a = dot2_acc(__builtin_amdgcn_perm(v.y, v.y, sel), a);
+            a = dot2_acc(__builtin_amdgcn_perm(v.z, v.z, sel), a);
+            a = dot2_acc(__builtin_amdgcn_perm(v.w, v.w, sel), a);
+        }
+#pragma unroll
+        for (int off = 1; off < S; off <<= 1) a += __shfl_xor(a, off, 64);
+        acc[p] = a;
+    }
+    // packets longer than S x K chunks: the whole wave, one packet at a time
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        uint64_t big = __builtin_amdgcn_ballot_w64(sub == 0u && nch[p] > (uint32_t)(S * K));
+        while (big) {
+            const uint32_t q = (uint32_t)__builtin_ctzll(big);
+            big &= big - 1ull;
+            const uint64_t qa0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(a0[p] >> 32), (int)q) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0[p], (int)q);
+            const uint32_t qlo = (uint32_t)__builtin_amdgcn_readlane((int)lo[p], (int)q);
+            const uint32_t qn = (uint32_t)__builtin_amdgcn_readlane((int)nch[p], (int)q);
+            const uint32_t qlv = (uint32_t)__builtin_amdgcn_readlane((int)lastv[p], (int)q);
+            const uint4* src = reinterpret_cast<const uint4*>(qa0);
+            uint32_t w = (qlo & 1u) ? wave_packet_sum<4, true>(src, qn, (int)qlo, qlv, lane)
+                                    : wave_packet_sum<4, false>(src, qn, (int)qlo, qlv, lane);
+            w = wave_sum_dpp(w);
+            if (lane == q) acc[p] = w;
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const uint32_t i = i0 + PB * p;
+        if (sub == 0u && i < n) out[i] = finish(dd[p].w, acc[p]);
+    }
+}
 }  // namespace lvlip
 
 // ======================================================== host side (C ABI) ==
@@ -1515,6 +1618,33 @@ bool launch_wflat(int waves_per_cu, hipStream_t s, const void* base, const lvlip
     }
 }
 
+// k_lane: S lanes per packet, P packets per lane group, K chunks per lane;
+// one launch wave.
+template <int S, int P, int K>
+void launch_lane_spk(hipStream_t s, const void* base, const lvlip_csum_desc* d, uint32_t n,
+                     uint16_t* out) {
+    constexpr uint64_t per_block = 256 / S * P;
+    const uint32_t grid = (uint32_t)(((uint64_t)n + per_block - 1) / per_block);
+    hipLaunchKernelGGL((lvlip::k_lane<S, P, K>), dim3(grid), dim3(256), 0, s, (const uint8_t*)base,
+                       d, n, out);
+}
+
+bool launch_lane(int lanes, int per_group, int chunks, hipStream_t s, const void* base,
+                 const lvlip_csum_desc* d, uint32_t n, uint16_t* out) {
+    switch ((lanes << 16) | (chunks << 8) | per_group) {
+#define LVLIP_LANE(SS, PP, KK) \
+    case (SS << 16) | (KK << 8) | PP: launch_lane_spk<SS, PP, KK>(s, base, d, n, out); return true;
+        LVLIP_LANE(1, 2, 4) LVLIP_LANE(1, 4, 4) LVLIP_LANE(1, 2, 6)
+        LVLIP_LANE(2, 2, 2) LVLIP_LANE(2, 4, 2) LVLIP_LANE(2, 4, 1) LVLIP_LANE(2, 8, 1)
+        LVLIP_LANE(2, 2, 4)
+        LVLIP_LANE(4, 2, 1) LVLIP_LANE(4, 4, 1) LVLIP_LANE(4, 8, 1) LVLIP_LANE(4, 2, 2)
+        LVLIP_LANE(4, 4, 2)
+        LVLIP_LANE(8, 4, 1) LVLIP_LANE(8, 2, 2) LVLIP_LANE(8, 4, 2)
+#undef LVLIP_LANE
+        default: return false;
+    }
+}
+
 template <int U>
 void launch_wave_lds(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
                      uint32_t n, uint16_t* out) {
@@ -1551,6 +1681,16 @@ int lvlip_device_count(void) {
 }  // extern "C"
 
 namespace {
+
+// AUTO's k_lane range: hints below this many bytes (scripts/shape_sweep.py,
+// DESIGN.md §4).  LVLIP_LANE_HINT_MAX overrides it (A/B knob, read once).
+int lane_hint_max() {
+    static const int v = [] {
+        const char* e = getenv("LVLIP_LANE_HINT_MAX");
+        return e ? atoi(e) : 33;
+    }();
+    return v;
+}
 
 // One launch of the selected kernel over n <= kLaunchMax descriptors.
 int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uint16_t* out,
@@ -1590,6 +1730,14 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             // 2 below 40 B (IPv4 headers alone, 20 B: 2 356 vs 2 251 with 4)
             kernel = LVLIP_KERNEL_FLAT;
             if (unroll <= 0 && hint > 0 && hint < 320) unroll = hint < 40 ? 2 : 4;
+            // up to 32 B (IPv4 headers alone, 20-32 B in 32-B slots): two
+            // lanes per packet read every slot pair as one contiguous wave
+            // load, no tile plan (20 / 32 B: 2 819 / 4 356 vs 2 474 / 4 121
+            // GB/s for the flat sweep; 36 B: 3 108 vs 3 469)
+            if (hint > 0 && hint < lane_hint_max()) {
+                kernel = LVLIP_KERNEL_LANE;
+                unroll = 0;
+            }
         }
     }
 
@@ -1647,6 +1795,19 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
                 default: break;
             }
             if (!ok) return LVLIP_EINVAL;
+            break;
+        }
+        case LVLIP_KERNEL_LANE: {
+            // unroll = packets per lane group (low byte, default 4) | chunks per
+            // lane << 8 (default 2) | lanes per packet << 16 (1, 2, 4 or 8;
+            // default 2): the default sums any packet of <= 49 B in its group
+            // (20-B headers at any alignment)
+            if (unroll < 0 || (unroll >> 24) != 0) return LVLIP_EINVAL;
+            int pg = unroll & 0xff, ch = (unroll >> 8) & 0xff, sl = (unroll >> 16) & 0xff;
+            if (pg == 0) pg = 4;
+            if (ch == 0) ch = 2;
+            if (sl == 0) sl = 2;
+            if (!launch_lane(sl, pg, ch, s, base, descs, n, out)) return LVLIP_EINVAL;
             break;
         }
         case LVLIP_KERNEL_WAVE_SIMPLE: {

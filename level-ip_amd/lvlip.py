@@ -29,11 +29,11 @@ LAB_PATH = os.path.join(HERE, "liblvlip_lab.so")
 # error codes (include/lvlip_csum.h)
 OK, EINVAL, ENODEV, EHIP, ENOMEM, ERANGE = 0, -1, -2, -3, -4, -5
 KERNEL_AUTO, KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_FLAT, KERNEL_WAVE_SIMPLE = 0, 1, 2, 3, 4
-KERNEL_WINDOW, KERNEL_WFLAT = 8, 9  # (6, 7: retired round-1 A/B ids, run WAVE)
+KERNEL_WINDOW, KERNEL_WFLAT, KERNEL_LANE = 8, 9, 10  # (6, 7: retired round-1 A/B ids, run WAVE)
 REG_DMA, REG_ZEROCOPY = 0, 1
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "wave_lds": KERNEL_WAVE_LDS,
                 "flat": KERNEL_FLAT, "wave_simple": KERNEL_WAVE_SIMPLE, "flat_v1": 5,
-                "window": KERNEL_WINDOW, "wflat": KERNEL_WFLAT}
+                "window": KERNEL_WINDOW, "wflat": KERNEL_WFLAT, "lane": KERNEL_LANE}
 
 # struct lvlip_csum_desc {u64 offset; i32 len; u32 start_sum;}  (16 B)
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<i4"), ("start_sum", "<u4")])

@@ -50,6 +50,10 @@ VARIANTS = [
     (lvlip.KERNEL_WFLAT, 0, 0),    # flat sweep per wave, tiles dealt round robin
     (lvlip.KERNEL_WFLAT, 2 | (16 << 8), 1),
     (lvlip.KERNEL_WFLAT, 8 | (64 << 8), 16),
+    (lvlip.KERNEL_LANE, 0, 0),     # S lanes per packet, longer packets to the wave
+    (lvlip.KERNEL_LANE, 2 | (6 << 8) | (1 << 16), 0),
+    (lvlip.KERNEL_LANE, 8 | (1 << 8) | (4 << 16), 0),
+    (lvlip.KERNEL_LANE, 4 | (2 << 8) | (8 << 16), 0),
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
@@ -224,7 +228,7 @@ def test_full_size_bit_exact(name):
                     (lvlip.KERNEL_WFLAT, 0, 0), (lvlip.KERNEL_WFLAT, 8 | (64 << 8), 16),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
-                    (lvlip.KERNEL_AUTO, 0, 0)]:
+                    (lvlip.KERNEL_LANE, 0, 0), (lvlip.KERNEL_AUTO, 0, 0)]:
         assert np.array_equal(run(base, descs, variant, out), want), variant
     # adversarial packets really are there and fold as the reference does
     ones = b.paint == 2
@@ -289,6 +293,60 @@ def test_wflat_tiles(tile):
             assert bad.size == 0, (n, u, wpc, bad[:5])
 
 
+# (lanes per packet S, packets per group P, chunks per lane K): every built shape
+LANE_SHAPES = [(1, 2, 4), (1, 4, 4), (1, 2, 6), (2, 2, 2), (2, 4, 2), (2, 4, 1), (2, 8, 1),
+               (2, 2, 4), (4, 2, 1), (4, 4, 1), (4, 8, 1), (4, 2, 2), (4, 4, 2), (8, 4, 1),
+               (8, 2, 2), (8, 4, 2)]
+
+
+def tiny_batch(seed, n_max=70000):
+    """Mostly tiny packets (0-80 B, odd lengths) at every byte offset, packed
+    with random gaps, plus 2 % of 81-3000 B, 0.1 % 64 KiB, 1 % negative
+    lengths; and the oracle's checksums."""
+    rng = np.random.default_rng(seed)
+    ln = rng.integers(0, 81, n_max).astype(np.int32)
+    r = rng.random(n_max)
+    ln[r < 0.02] = rng.integers(81, 3000, int((r < 0.02).sum()))
+    ln[rng.random(n_max) < 0.001] = 65535
+    ln[rng.random(n_max) < 0.01] = -7
+    off = np.zeros(n_max, dtype=np.uint64)
+    off[1:] = np.cumsum(np.maximum(ln, 0)[:-1] + rng.integers(0, 17, n_max - 1))
+    off += 3
+    blob = rng.integers(0, 256, int(off[-1]) + max(int(ln[-1]), 0) + 64, dtype=np.uint8)
+    st = rng.integers(0, 2**32, n_max, dtype=np.uint64).astype(np.uint32)
+    d = mk_descs(off, ln, st)
+    return dev_blob(blob), d, pyoracle.batch(blob, d, threads=THREADS)
+
+
+@pytest.mark.parametrize("shape", LANE_SHAPES, ids=[f"s{s}p{p}k{k}" for s, p, k in LANE_SHAPES])
+def test_lane_shapes(shape):
+    """k_lane for every built shape (lanes per packet, packets per group, chunks
+    per lane), on
+    batch sizes that leave the last block short; tiny packets at every byte
+    offset next to packets too long for the lane (the wave loop: up to 64 KiB),
+    empty and negative lengths; every output against the oracle."""
+    sl, p, k = shape
+    base, d, want = tiny_batch(200 + 64 * sl + 8 * p + k)
+    for n in BATCH_SIZES:
+        out = lvlip.batch_torch(base, dev_descs(d[:n]), kernel=lvlip.KERNEL_LANE,
+                                unroll=p | (k << 8) | (sl << 16))
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint16)
+        bad = np.nonzero(got != want[:n])[0]
+        assert bad.size == 0, (n, bad[:5], [(int(d["offset"][i]), int(d["len"][i])) for i in bad[:5]])
+
+
+def test_auto_small_hints():
+    """AUTO with small length hints (k_lane up to 32 B, the flat sweep above),
+    on tiny packets next to long ones; against the oracle."""
+    base, d, want = tiny_batch(7)
+    descs = dev_descs(d)
+    for hint in (1, 20, 32, 33, 40, 64):
+        out = lvlip.batch_torch(base, descs, len_hint=hint)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint16), want), hint
+
+
 def test_config5_96gb_chunked():
     """BASELINE config #5 on one GPU: 64 M x 1500 B = 96 GB in HBM (offsets far
     past 2^32).  Every output is compared with the oracle over the same bytes,
@@ -345,7 +403,10 @@ def test_bad_launch_shapes_rejected():
     descs = dev_descs(mk_descs([0], [4], [0]))
     out = torch.empty(1, dtype=torch.int16, device="cuda")
     for k, u in ((lvlip.KERNEL_FLAT, 3), (lvlip.KERNEL_FLAT, 8 | (4 << 8)),
-                 (lvlip.KERNEL_WINDOW, 2 | (5 << 8)), (lvlip.KERNEL_WFLAT, 8 | (48 << 8))):
+                 (lvlip.KERNEL_WINDOW, 2 | (5 << 8)), (lvlip.KERNEL_WFLAT, 8 | (48 << 8)),
+                 (lvlip.KERNEL_LANE, 3), (lvlip.KERNEL_LANE, 4 | (5 << 8)),
+                 (lvlip.KERNEL_LANE, 4 | (1 << 8) | (3 << 16)),
+                 (lvlip.KERNEL_LANE, 4 | (1 << 8) | (1 << 24))):
         with pytest.raises(lvlip.LvlipError):
             lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None, k, u, 0, 0)
 
@@ -560,7 +621,8 @@ def test_max_int_packet():
     for variant in [(lvlip.KERNEL_AUTO, 0, 0), (lvlip.KERNEL_WAVE, 2, 0), (lvlip.KERNEL_FLAT, 0, 0),
                     (lvlip.KERNEL_FLAT, 4 | (2 << 8), 0), (lvlip.KERNEL_WINDOW, 2 | (3 << 8), 0),
                     (lvlip.KERNEL_WINDOW, 3 | (1 << 8), 1), (lvlip.KERNEL_WFLAT, 0, 0),
-                    (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0)]:
+                    (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
+                    (lvlip.KERNEL_LANE, 0, 0), (lvlip.KERNEL_LANE, 2 | (4 << 8) | (1 << 16), 0)]:
         assert list(run(base, descs, variant)) == list(want), variant
     # AUTO with the caller's hint (the batch's average length: k_window, G 3)
     out = lvlip.batch_torch(base, descs, None, len_hint=(n1 + (1 << 30)) // 2)
