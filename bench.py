@@ -427,9 +427,14 @@ def frames_dev(lvlip, torch, dev):
     for name, fn, nbytes in (
             ("tx_fill", lambda: lvlip.tx_checksum_dev(base, fdt, stream=stream), 20 * n + l4_bytes),
             ("rx_header", lambda: lvlip.rx_verify_dev(base, fdt, 0, stream=stream), 20 * n),
+            # the header call's A/B kernel (k_flat2 with a frame source)
+            ("rx_header_flat", lambda: lvlip.rx_verify_dev(base, fdt, 0, stream=stream), 20 * n),
             ("rx_header_l4", lambda: lvlip.rx_verify_dev(base, fdt, lvlip.RX_VERIFY_L4, stream=stream),
              20 * n + l4_bytes)):
+        if name == "rx_header_flat":
+            os.environ["LVLIP_FRAMES_RX_HDR"] = "flat"
         ms = timed(torch, fn, stream, reps=10)
+        os.environ.pop("LVLIP_FRAMES_RX_HDR", None)
         res[name] = {"ms": round(ms, 4), "Mframes_per_s": round(n / ms / 1e3, 1),
                      "GBps": round(nbytes / ms / 1e6, 1)}
     v = lvlip.rx_verify_dev(base, fdt, 0, stream=stream)

@@ -1417,6 +1417,47 @@ __global__ __launch_bounds__(256) void k_lane(const uint8_t* __restrict__ base,
         if (sub == 0u && i < n) out[i] = finish(dd[p].w, acc[p]);
     }
 }
+
+// --------------------------------------------- k_rx_hdr (RX header verify) --
+//
+// f1's header-only RX call (lvlip_rx_verify_dev without LVLIP_RX_VERIFY_L4) as
+// one lane per frame.  The parse window FrWin already holds frame bytes
+// [12, 56): the whole IPv4 header for ihl <= 10, so the lane sums it from
+// registers (header dword m = window bytes 14+4m .. 17+4m, one alignbyte each)
+// and no entry, tile plan or second read of the header exists.  Headers with
+// more options (ihl 11-15) read their last words with byte loads.  The
+// decisions are FrameSrc<FR_RX>'s (parse_rx) and the verdict rule its put's.
+__global__ __launch_bounds__(256) void k_rx_hdr(const uint8_t* __restrict__ base,
+                                                const lvlip_frame_desc* __restrict__ frames,
+                                                uint32_t n, uint8_t* __restrict__ verdict) {
+    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
+    if (f >= n) return;  // no cross-lane step below
+    const FrameSrc<FR_RX> src{base, nullptr, frames, verdict};
+    const uint4 raw = load_global(reinterpret_cast<uint64_t>(frames + f));
+    lvlip_frame_desc fd;
+    fd.offset = ((uint64_t)raw.y << 32) | raw.x;
+    fd.len = raw.z;
+    fd.reserved = 0;
+    const uint8_t* h = base + fd.offset;
+    FrWin x;
+    x.load(h, fd.len, reinterpret_cast<uint64_t>(frames + f) & ~15ull);
+    lvlip_csum_desc d0 = fr_mk(0, 0, 0), d1 = fr_mk(0, 0, 0);
+    uint32_t w = 0;
+    src.parse_rx(fd, x, d0, d1, w);
+    uint32_t v = w & 0xffu;
+    if (w & FR_HAS_HDR) {
+        const uint32_t ihl = x.b(14) & 0x0fu;
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t m = 0; m < 10u; ++m)
+            acc = dot2_acc(m < ihl ? __builtin_amdgcn_alignbyte(x.A[m + 1u], x.A[m], 2u) : 0u, acc);
+        for (uint32_t k = 54u; k < FR_ETH + 4u * ihl; k += 2u) acc += fr_le16(h + k);
+        // src/ip_input.c:38-43, as FrameSrc<FR_RX>::put
+        if (finish(0u, acc) != 0u) v = LVLIP_RX_BAD_CSUM;
+        v = v == 0u ? (uint32_t)LVLIP_RX_OK : (v & ~FR_PENDING);
+    }
+    verdict[f] = (uint8_t)v;
+}
 }  // namespace lvlip
 
 // ======================================================== host side (C ABI) ==
@@ -1931,9 +1972,32 @@ bool frames_quarters() {
     return q;
 }
 
+// LVLIP_FRAMES_RX_HDR (A/B knob, read per call so one process can time and
+// test both): the header-only RX call's kernel, lane (default: k_rx_hdr, one
+// lane per frame) | flat (k_flat2 with a frame source, as the other frame
+// calls).
+bool frames_rx_lane() {
+    const char* e = getenv("LVLIP_FRAMES_RX_HDR");
+    return !(e && strcmp(e, "flat") == 0);
+}
+
+int launch_rx_hdr(const void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* out8,
+                  hipStream_t s) {
+    for (uint32_t f0 = 0; f0 < n;) {
+        const uint32_t m = n - f0 < kLaunchMax ? n - f0 : kLaunchMax;
+        hipLaunchKernelGGL(lvlip::k_rx_hdr, dim3((m + 255u) / 256u), dim3(256), 0, s,
+                           (const uint8_t*)base, frames + f0, m, out8 + f0);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "k_rx_hdr");
+        f0 += m;
+    }
+    return LVLIP_OK;
+}
+
 template <int MODE>
 int launch_frames(const void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* out8,
                   hipStream_t s) {
+    if (MODE == lvlip::FR_RX && frames_rx_lane()) return launch_rx_hdr(base, frames, n, out8, s);
     using Src = lvlip::FrameSrc<MODE>;
     // a dispatch holds at most 2^30 entries (kLaunchMax): whole frames per launch
     const uint32_t per = kLaunchMax / Src::SLOTS;

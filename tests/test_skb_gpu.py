@@ -233,3 +233,30 @@ def test_rx_verify_agrees_with_reference_ip_rcv(ctx):
     accepted = [f for f, v in zip(frs, got) if v == lvlip.RX_OK]
     assert ref_rx_cases.reference_replies(accepted) == [r for r, v in zip(replies, got)
                                                         if v == lvlip.RX_OK]
+
+
+def test_rx_header_lane_and_flat_agree(monkeypatch):
+    """The header-only RX call on both of its kernels (k_rx_hdr, one lane per
+    frame, the default; k_flat2 with a frame source, LVLIP_FRAMES_RX_HDR=flat):
+    20 000 frames at every alignment, 20 % with IP options (ihl 6-15, the
+    window's last words and the byte-load tail), a tenth with a flipped bit in
+    the header or beyond, some truncated; every verdict == the oracle's."""
+    fr = workloads.frames(20000, seed=61, max_l4=1460)
+    for f in fr:
+        skb_oracle.tx_fill(f)
+    rng = np.random.default_rng(62)
+    for i in rng.choice(len(fr), 2000, replace=False):
+        f = fr[int(i)]
+        ihl = f[14] & 0xF
+        f[14 + int(rng.integers(0, ihl * 4 + 8))] ^= 1 << int(rng.integers(0, 8))
+    for i in rng.choice(len(fr), 200, replace=False):
+        fr[int(i)] = fr[int(i)][: int(rng.integers(0, 80))]
+    want = [skb_oracle.rx_verdict(f, 0) for f in fr]
+    buf, fd = lvlip.pack_frames(fr, align_mod=16, seed=4)
+    base = _dev(buf)
+    for kern in ("lane", "flat"):
+        monkeypatch.setenv("LVLIP_FRAMES_RX_HDR", kern)
+        got = lvlip.rx_verify_dev(base, fd, 0).cpu().numpy()
+        bad = np.nonzero(got != np.array(want, dtype=np.uint8))[0]
+        assert bad.size == 0, (kern, bad[:5])
+    assert len(set(want)) >= 3
