@@ -1,14 +1,14 @@
 #!/usr/bin/env python3
-"""Summarise a scripts/profile.sh run of `bench.py --frames` (KRE=k_flat2) into
-profiles/<tag>_frames_pmc.json: per device frame call (TX fill, RX header, RX
-header + L4) the kernel's median duration, HBM bytes from the PMC passes, and the
-algorithmic bytes.
+"""Summarise a scripts/profile.sh run of `bench.py --frames` (KRE="k_flat2|k_rx_hdr")
+into profiles/<tag>_frames_pmc.json: per device frame call (TX fill, RX header on
+k_rx_hdr and on k_flat2, RX header + L4) the kernel's median duration, HBM bytes
+from the PMC passes, and the algorithmic bytes.
 
-The trace names every frame launch `k_flat2` (truncated), so calls are told
-apart by order: bench.py's frames_dev times tx_fill, rx_header, rx_header_l4,
-each 3 warm-ups + 10 reps, then one rx_header for the all-OK check.  That order
-is checked against the grid sizes (RX header-only uses one slot per frame, the
-others two).
+The trace names every flat frame launch `k_flat2` (truncated), so calls are told
+apart by order: bench.py's frames_dev times tx_fill, rx_header (k_rx_hdr),
+rx_header_flat (k_flat2), rx_header_l4, each 3 warm-ups + 10 reps, then one
+rx_header for the all-OK check.  That order is checked against the kernel names
+and grid sizes (RX header-only uses one slot per frame, the others two).
 
 hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, as scripts/prof_summary.py.
 Algorithmic bytes: the checksummed bytes (20 B per header + the L4 bytes) plus
@@ -27,11 +27,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "level-ip_amd"))
 import workloads  # noqa: E402
 
-MODES = ["tx_fill"] * 13 + ["rx_header"] * 13 + ["rx_header_l4"] * 13 + ["rx_header"]
+MODES = (["tx_fill"] * 13 + ["rx_header"] * 13 + ["rx_header_flat"] * 13 + ["rx_header_l4"] * 13
+         + ["rx_header"])
+KERNEL = {"tx_fill": "k_flat2", "rx_header": "k_rx_hdr", "rx_header_flat": "k_flat2",
+          "rx_header_l4": "k_flat2"}
 
 
 def dispatches(path, value_col=None):
-    rows = [r for r in csv.DictReader(open(path)) if r["Kernel_Name"].startswith("k_flat2")]
+    rows = [r for r in csv.DictReader(open(path)) if r["Kernel_Name"].startswith(("k_flat2", "lvlip::k_flat2",
+                                                                                   "k_rx_hdr", "lvlip::k_rx_hdr"))]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     return rows
 
@@ -41,16 +45,19 @@ def main():
     b = workloads.make("mixed")
     n = b.descs.size // 2
     l4 = int(b.descs[1::2]["len"].sum())
-    algo = {"tx_fill": 20 * n + l4 + 5 * n, "rx_header": 20 * n + n, "rx_header_l4": 20 * n + l4 + n}
+    algo = {"tx_fill": 20 * n + l4 + 5 * n, "rx_header": 20 * n + n, "rx_header_flat": 20 * n + n,
+            "rx_header_l4": 20 * n + l4 + n}
     # the device calls come first; later k_flat2 launches (the host-API timings
     # of bench.py --frames) are not part of this summary
     trace = dispatches(os.path.join(prof, "trace", "trace_kernel_trace.csv"))[: len(MODES)]
     assert len(trace) == len(MODES), (len(trace), len(MODES))
     per = {m: {"dur_ns": [], "grid": set()} for m in algo}
     for r, m in zip(trace, MODES):
+        assert KERNEL[m] in r["Kernel_Name"], (m, r["Kernel_Name"])
         per[m]["dur_ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         per[m]["grid"].add(int(r["Grid_Size_X"]))
     assert per["rx_header"]["grid"] == {256 * ((n + 255) // 256)}, per["rx_header"]["grid"]
+    assert per["rx_header_flat"]["grid"] == {256 * ((n + 255) // 256)}, per["rx_header_flat"]["grid"]
     for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         rows = dispatches(os.path.join(prof, sub, f"{sub}_counter_collection.csv"))[: len(MODES)]
         assert len(rows) == len(MODES), (sub, len(rows))
