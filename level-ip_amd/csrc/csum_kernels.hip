@@ -1336,7 +1336,7 @@ __global__ __launch_bounds__(256) void k_wflat(const uint8_t* __restrict__ base,
 // within u16 halves (see the file header).  A packet longer than S x K
 // chunks is summed by the whole wave after the group phase
 // (wave_packet_sum), one packet at a time.
-template <int S, int P, int K>
+template <int S, int P, int K, int M>
 __global__ __launch_bounds__(256) void k_lane(const uint8_t* __restrict__ base,
                                               const lvlip_csum_desc* __restrict__ descs,
                                               uint32_t n, uint16_t* __restrict__ out) {
@@ -1349,8 +1349,22 @@ __global__ __launch_bounds__(256) void k_lane(const uint8_t* __restrict__ base,
 #pragma unroll
     for (int p = 0; p < P; ++p) {
         const uint32_t i = i0 + PB * p;
-        dd[p] = i < n ? load_global(reinterpret_cast<uint64_t>(descs + i)) : make_uint4(0u, 0u, 0u, 0u);
+        if (M == 0) {
+            dd[p] = i < n ? load_global(reinterpret_cast<uint64_t>(descs + i)) : make_uint4(0u, 0u, 0u, 0u);
+        } else {
+            const uint4 v = load_global(reinterpret_cast<uint64_t>(descs + (i < n ? i : n - 1u)));
+            dd[p] = i < n ? v : make_uint4(0u, 0u, 0u, 0u);
+        }
     }
+    // Chunk loads, M = 0 (default): only the lanes with a chunk to read load
+    // (exec-masked).  hipcc turns each conditional load into a branch and
+    // retires each packet's K loads at the join, so a lane has K chunks in
+    // flight at a time.  M = 1 (A/B): every lane loads unconditionally, a lane
+    // with nothing to read from one wave-uniform address (the descriptor
+    // array's first 16 B), and all P x K loads are issued before any is used
+    // (sched_barrier).  Measured, M = 0 is faster: the masked lanes cost the
+    // address unit nothing, and enough waves cover the latency.
+    const uint64_t safe = reinterpret_cast<uint64_t>(descs);
     uint64_t a0[P];
     uint32_t lo[P], nch[P], lastv[P];
     uint4 x[P][K];
@@ -1367,22 +1381,28 @@ __global__ __launch_bounds__(256) void k_lane(const uint8_t* __restrict__ base,
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = sub + (uint32_t)(S * k);
-            x[p][k] = (in_group && c < nch[p]) ? load_nt_global(a0[p] + 16ull * c)
-                                               : make_uint4(0u, 0u, 0u, 0u);
+            const bool want = in_group && c < nch[p];
+            if (M == 0)
+                x[p][k] = want ? load_nt_global(a0[p] + 16ull * c) : make_uint4(0u, 0u, 0u, 0u);
+            else
+                x[p][k] = load_nt_global(want ? a0[p] + 16ull * c : safe);
         }
     }
+    if (M == 1) __builtin_amdgcn_sched_barrier(0);
     uint32_t acc[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) {
         const uint32_t sel = (lo[p] & 1u) ? 0x02030001u : 0x03020100u;
+        const bool in_group = nch[p] <= (uint32_t)(S * K);
         uint32_t a = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t c = sub + (uint32_t)(S * k);
-            uint4 v = x[p][k];
+            uint4 v = M == 0 || (in_group && c < nch[p]) ? x[p][k] : make_uint4(0u, 0u, 0u, 0u);
             const int b0 = c == 0u ? (int)lo[p] : 0;
             const int b1 = c + 1u == nch[p] ? (int)lastv[p] : 16;
-            if (c == 0u || c + 1u == nch[p]) v = mask_chunk(v, b0, b1);
+            // M = 1: unconditional (no branch), all-ones masks for the middle chunks
+            if (M == 1 || c == 0u || c + 1u == nch[p]) v = mask_chunk(v, b0, b1);
             a = dot2_acc(__builtin_amdgcn_perm(v.x, v.x, sel), a);
             a = dot2_acc(__builtin_amdgcn_perm(v.y, v.y, sel), a);
             a = dot2_acc(__builtin_amdgcn_perm(v.z, v.z, sel), a);
@@ -1662,19 +1682,23 @@ bool launch_wflat(int waves_per_cu, hipStream_t s, const void* base, const lvlip
 // k_lane: S lanes per packet, P packets per lane group, K chunks per lane;
 // one launch wave.
 template <int S, int P, int K>
-void launch_lane_spk(hipStream_t s, const void* base, const lvlip_csum_desc* d, uint32_t n,
+void launch_lane_spk(int mode, hipStream_t s, const void* base, const lvlip_csum_desc* d, uint32_t n,
                      uint16_t* out) {
     constexpr uint64_t per_block = 256 / S * P;
     const uint32_t grid = (uint32_t)(((uint64_t)n + per_block - 1) / per_block);
-    hipLaunchKernelGGL((lvlip::k_lane<S, P, K>), dim3(grid), dim3(256), 0, s, (const uint8_t*)base,
-                       d, n, out);
+    if (mode)
+        hipLaunchKernelGGL((lvlip::k_lane<S, P, K, 1>), dim3(grid), dim3(256), 0, s,
+                           (const uint8_t*)base, d, n, out);
+    else
+        hipLaunchKernelGGL((lvlip::k_lane<S, P, K, 0>), dim3(grid), dim3(256), 0, s,
+                           (const uint8_t*)base, d, n, out);
 }
 
-bool launch_lane(int lanes, int per_group, int chunks, hipStream_t s, const void* base,
+bool launch_lane(int lanes, int per_group, int chunks, int mode, hipStream_t s, const void* base,
                  const lvlip_csum_desc* d, uint32_t n, uint16_t* out) {
     switch ((lanes << 16) | (chunks << 8) | per_group) {
 #define LVLIP_LANE(SS, PP, KK) \
-    case (SS << 16) | (KK << 8) | PP: launch_lane_spk<SS, PP, KK>(s, base, d, n, out); return true;
+    case (SS << 16) | (KK << 8) | PP: launch_lane_spk<SS, PP, KK>(mode, s, base, d, n, out); return true;
         LVLIP_LANE(1, 2, 4) LVLIP_LANE(1, 4, 4) LVLIP_LANE(1, 2, 6)
         LVLIP_LANE(2, 2, 2) LVLIP_LANE(2, 4, 2) LVLIP_LANE(2, 4, 1) LVLIP_LANE(2, 8, 1)
         LVLIP_LANE(2, 2, 4)
@@ -1841,14 +1865,16 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         case LVLIP_KERNEL_LANE: {
             // unroll = packets per lane group (low byte, default 4) | chunks per
             // lane << 8 (default 2) | lanes per packet << 16 (1, 2, 4 or 8;
-            // default 2): the default sums any packet of <= 49 B in its group
-            // (20-B headers at any alignment)
-            if (unroll < 0 || (unroll >> 24) != 0) return LVLIP_EINVAL;
+            // default 2) | load mode << 24 (0 masked, 1 unconditional: A/B):
+            // the default sums any packet of <= 49 B in its group (20-B
+            // headers at any alignment)
+            if (unroll < 0 || (unroll >> 25) != 0) return LVLIP_EINVAL;
             int pg = unroll & 0xff, ch = (unroll >> 8) & 0xff, sl = (unroll >> 16) & 0xff;
+            const int mode = (unroll >> 24) & 1;
             if (pg == 0) pg = 4;
             if (ch == 0) ch = 2;
             if (sl == 0) sl = 2;
-            if (!launch_lane(sl, pg, ch, s, base, descs, n, out)) return LVLIP_EINVAL;
+            if (!launch_lane(sl, pg, ch, mode, s, base, descs, n, out)) return LVLIP_EINVAL;
             break;
         }
         case LVLIP_KERNEL_WAVE_SIMPLE: {

@@ -11,7 +11,8 @@ env: SH_LENS (default 512,768,1024,1500,2048,3000,4096,9000),
      SH_TOTAL (bytes of packet slots per length, default 1.5e9),
      SH_FLAT (k_flat2 unrolls, e.g. 8,4; default none),
      SH_WFLAT (k_wflat shapes UxWxD: loads per round, waves/CU, descriptors per tile),
-     SH_LANE (k_lane shapes SxPxK: lanes per packet, packets per group, chunks per lane)
+     SH_LANE (k_lane shapes SxPxK[xM]: lanes per packet, packets per group, chunks per lane,
+              load mode)
 writes JSON to argv[1]."""
 import json
 import os
@@ -72,8 +73,9 @@ def main():
             u, w, dd = (int(v) for v in sh.split("x"))
             variants.append(("wflat", u | (dd << 8), w))
         for sh in filter(None, os.environ.get("SH_LANE", "").split(",")):
-            sl, pl, ch = (int(v) for v in sh.split("x"))
-            variants.append(("lane", pl | (ch << 8) | (sl << 16), 0))
+            v = [int(t) for t in sh.split("x")]
+            sl, pl, ch, md = v + [0] * (4 - len(v))
+            variants.append(("lane", pl | (ch << 8) | (sl << 16) | (md << 24), 0))
         for _ in range(rounds):
             for k, r, w in variants:
                 def f():
@@ -81,7 +83,8 @@ def main():
                                     lvlip.KERNEL_NAMES[k], r, w, L)
                 ms = timed(f, s)
                 key = f"{k}-{r & 0xff}x{w}" + (f"g{(r >> 8) & 0xff}" if r >> 8 else "")  # g = group / tile
-                key += f"s{r >> 16}" if r >> 16 else ""  # k_lane: lanes per packet
+                key += f"s{(r >> 16) & 0xff}" if r >> 16 else ""  # k_lane: lanes per packet
+                key += f"m{r >> 24}" if r >> 24 else ""  # k_lane: load mode
                 row.setdefault(key, []).append(round(algo / ms / 1e6, 1))
         best = max(row, key=lambda k: max(row[k]))
         print(f"L={L:5d} n={n:8d} " + "  ".join(f"{k}:{max(v):7.1f}" for k, v in row.items()) + f"  best {best}",

@@ -318,10 +318,11 @@ def tiny_batch(seed, n_max=70000):
     return dev_blob(blob), d, pyoracle.batch(blob, d, threads=THREADS)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("shape", LANE_SHAPES, ids=[f"s{s}p{p}k{k}" for s, p, k in LANE_SHAPES])
-def test_lane_shapes(shape):
+def test_lane_shapes(shape, mode):
     """k_lane for every built shape (lanes per packet, packets per group, chunks
-    per lane), on
+    per lane) and both load modes, on
     batch sizes that leave the last block short; tiny packets at every byte
     offset next to packets too long for the lane (the wave loop: up to 64 KiB),
     empty and negative lengths; every output against the oracle."""
@@ -329,7 +330,7 @@ def test_lane_shapes(shape):
     base, d, want = tiny_batch(200 + 64 * sl + 8 * p + k)
     for n in BATCH_SIZES:
         out = lvlip.batch_torch(base, dev_descs(d[:n]), kernel=lvlip.KERNEL_LANE,
-                                unroll=p | (k << 8) | (sl << 16))
+                                unroll=p | (k << 8) | (sl << 16) | (mode << 24))
         torch.cuda.synchronize()
         got = out.cpu().numpy().view(np.uint16)
         bad = np.nonzero(got != want[:n])[0]
@@ -406,7 +407,7 @@ def test_bad_launch_shapes_rejected():
                  (lvlip.KERNEL_WINDOW, 2 | (5 << 8)), (lvlip.KERNEL_WFLAT, 8 | (48 << 8)),
                  (lvlip.KERNEL_LANE, 3), (lvlip.KERNEL_LANE, 4 | (5 << 8)),
                  (lvlip.KERNEL_LANE, 4 | (1 << 8) | (3 << 16)),
-                 (lvlip.KERNEL_LANE, 4 | (1 << 8) | (1 << 24))):
+                 (lvlip.KERNEL_LANE, 4 | (1 << 8) | (1 << 25))):
         with pytest.raises(lvlip.LvlipError):
             lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None, k, u, 0, 0)
 
