@@ -149,7 +149,9 @@ typedef struct lvlip_launch_cfg {
                                per tile << 8 (16, 32 or 64; 0 = 32);
                                FLAT: 64-chunk loads per round | group order
                                << 8 (1 interleaved, 2 quarters, 3 blocks;
-                               0 = LVLIP_FLAT_GROUPS, else quarters);
+                               0 = LVLIP_FLAT_GROUPS, else quarters) | 1 << 10
+                               for tiles of 512 descriptors (A/B; U 4 or 8,
+                               quarters or blocks);
                                LANE: packets per lane group | 16-B chunks
                                per lane << 8 | lanes per packet << 16 (1, 2,
                                4, 8); longer packets go to a whole-wave

@@ -778,7 +778,6 @@ __global__ __launch_bounds__(FLAT_T) void k_flat(const uint8_t* __restrict__ bas
 // Packets longer than FCAP chunks go to a whole-wave loop instead.
 constexpr int FT = 256;                  // descriptors per tile = threads
 constexpr uint32_t FCAP = 128;           // chunks of the largest swept packet (2 KiB)
-constexpr uint32_t FGROUPS = FT * FCAP / 64;
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_row_shr(uint32_t v) {
@@ -834,67 +833,94 @@ __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
     return ((1u << w) - 1u) << (8 * s);
 }
 
-template <int U, bool NT, int GORD, class Src>
+// D descriptors per thread (a tile of FT * D): D = 2 halves the per-tile
+// plan's share of the launch (A/B, batch calls only; unroll bit 10).  Thread t
+// owns the tile's descriptors t*D .. t*D + D - 1, so its ranks, chunk starts
+// and big-packet slots follow from one exclusive scan of its D counts.
+template <int U, bool NT, int GORD, class Src, int D = 1>
 __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, const Src src,
                                               uint32_t n) {
-    __shared__ uint4 s_rec[FT];        // by rank: {a0 lo, a0 hi, cstart, meta}
-    __shared__ uint2 s_grp[FGROUPS];   // by 64-chunk group: head bitmap {lo, hi}
-    __shared__ uint16_t s_hb[FGROUPS]; // by 64-chunk group: heads before it (<= FT)
-    __shared__ uint32_t s_acc[FT];     // by descriptor
-    __shared__ uint32_t s_big[FT];     // descriptors longer than FCAP chunks
-    __shared__ uint4 s_edge[2 * FT];   // by descriptor: raw first / last chunk
+    static_assert(D == 1 || D == 2, "descriptors per thread");
+    constexpr uint32_t TD = (uint32_t)FT * D;   // descriptors per tile
+    constexpr uint32_t FG = TD * FCAP / 64;     // most 64-chunk groups a tile can have
+    __shared__ uint4 s_rec[TD];        // by rank: {a0 lo, a0 hi, cstart, meta}
+    __shared__ uint2 s_grp[FG];        // by 64-chunk group: head bitmap {lo, hi}
+    __shared__ uint16_t s_hb[FG];      // by 64-chunk group: heads before it (<= TD)
+    __shared__ uint32_t s_acc[TD];     // by descriptor
+    __shared__ uint32_t s_big[TD];     // descriptors longer than FCAP chunks
+    __shared__ uint4 s_edge[2 * TD];   // by descriptor: raw first / last chunk
     __shared__ uint32_t s_tmp[8];
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t tile0 = blockIdx.x * (uint32_t)FT;
+    const uint32_t tile0 = blockIdx.x * TD;
     const uint32_t t = tid;
-    const uint32_t i_me = tile0 + t;
 
     // ---- phase 1: descriptors -> chunk counts, ranks, records, head bitmap
-    uint32_t start_sum = 0, nch = 0, meta = 0, lo = 0, lastv = 16, ctx = 0;
-    uint64_t a0 = 0;  // the entry's first byte is a0 + lo
-    bool big = false;
-    if (i_me < n) {
-        const lvlip_csum_desc d = src.get(i_me, ctx);
-        start_sum = d.start_sum;
-        if (d.len > 0) {
-            const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
-            a0 = abs & ~15ull;
-            lo = (uint32_t)(abs & 15ull);
-            const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
-            const uint64_t c64 = (span + 15u) >> 4;
-            lastv = (uint32_t)(span - 16ull * (c64 - 1u));
-            const bool odd = abs & 1ull;
-            big = c64 > FCAP;
-            nch = big ? 0u : (uint32_t)c64;
-            // edge flags: the sweep stashes the packet's first (bit 10) and last
-            // (bit 11) chunk in LDS when they hold bytes outside the packet
-            const bool ef = !big && (lo != 0u || (c64 == 1u && lastv != 16u));
-            const bool el = !big && c64 > 1u && lastv != 16u;
-            meta = nch | ((uint32_t)odd << 9) | ((uint32_t)ef << 10) | ((uint32_t)el << 11) | (t << 18);
+    uint32_t start_sum[D], nch[D], meta[D], lo[D], lastv[D], ctx[D];
+    uint64_t a0[D];  // the entry's first byte is a0 + lo
+    bool big[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const uint32_t j = t * D + d, i = tile0 + j;
+        start_sum[d] = 0, nch[d] = 0, meta[d] = 0, lo[d] = 0, lastv[d] = 16, ctx[d] = 0;
+        a0[d] = 0;
+        big[d] = false;
+        if (i < n) {
+            const lvlip_csum_desc ds = src.get(i, ctx[d]);
+            start_sum[d] = ds.start_sum;
+            if (ds.len > 0) {
+                const uint64_t abs = reinterpret_cast<uint64_t>(base) + ds.offset;
+                a0[d] = abs & ~15ull;
+                lo[d] = (uint32_t)(abs & 15ull);
+                const uint64_t span = (uint64_t)lo[d] + (uint64_t)(uint32_t)ds.len;
+                const uint64_t c64 = (span + 15u) >> 4;
+                lastv[d] = (uint32_t)(span - 16ull * (c64 - 1u));
+                const bool odd = abs & 1ull;
+                big[d] = c64 > FCAP;
+                nch[d] = big[d] ? 0u : (uint32_t)c64;
+                // edge flags: the sweep stashes the packet's first (bit 10) and
+                // last (bit 11) chunk in LDS when they hold bytes outside it
+                const bool ef = !big[d] && (lo[d] != 0u || (c64 == 1u && lastv[d] != 16u));
+                const bool el = !big[d] && c64 > 1u && lastv[d] != 16u;
+                meta[d] = nch[d] | ((uint32_t)odd << 9) | ((uint32_t)ef << 10) | ((uint32_t)el << 11) |
+                          (j << 18);
+            }
         }
+        s_acc[j] = 0u;
     }
-    s_acc[t] = 0u;
-    for (uint32_t g = t; g < FGROUPS; g += FT) s_grp[g] = make_uint2(0u, 0u);
+    for (uint32_t g = t; g < FG; g += FT) s_grp[g] = make_uint2(0u, 0u);
     // one scan pass for three prefixes: big packets (high half) and swept
-    // packets (low half, both <= 256) packed in one word, chunks in the other
-    uint32_t e1 = 0, cstart = 0, t1 = 0, C = 0;
-    block_excl_scan2((big ? 0x10000u : 0u) | (nch ? 1u : 0u), nch, s_tmp, &e1, &cstart, &t1, &C);
-    const uint32_t big_pos = e1 >> 16, nbig = t1 >> 16;
-    const uint32_t rank = e1 & 0xffffu;
+    // packets (low half, both <= TD) packed in one word, chunks in the other
+    uint32_t sa = 0, sb = 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        sa += (big[d] ? 0x10000u : 0u) | (nch[d] ? 1u : 0u);
+        sb += nch[d];
+    }
+    uint32_t e1 = 0, cs = 0, t1 = 0, C = 0;
+    block_excl_scan2(sa, sb, s_tmp, &e1, &cs, &t1, &C);
+    const uint32_t nbig = t1 >> 16;
     const uint32_t G = (C + 63u) >> 6;
-    if (big) s_big[big_pos] = t;
-    if (nch) {
-        s_rec[rank] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), cstart, meta);
-        const uint32_t g = cstart >> 6, b = cstart & 63u;
-        if (b < 32u) atomicOr(&s_grp[g].x, 1u << b);
-        else atomicOr(&s_grp[g].y, 1u << (b - 32u));
-        // heads before group g = swept packets that start before chunk 64 g.
-        // The packets' chunk ranges tile [0, C) in rank order, so for every
-        // group that starts inside (cstart, cstart + nch] that count is this
-        // packet's rank + 1 (at most 3 groups: nch <= FCAP = 128)
-        for (uint32_t gg = g + 1u; gg < G && (gg << 6) <= cstart + nch; ++gg)
-            s_hb[gg] = (uint16_t)(rank + 1u);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const uint32_t j = t * D + d;
+        const uint32_t big_pos = e1 >> 16, rank = e1 & 0xffffu, cstart = cs;
+        if (big[d]) s_big[big_pos] = j;
+        if (nch[d]) {
+            s_rec[rank] = make_uint4((uint32_t)a0[d], (uint32_t)(a0[d] >> 32), cstart, meta[d]);
+            const uint32_t g = cstart >> 6, b = cstart & 63u;
+            if (b < 32u) atomicOr(&s_grp[g].x, 1u << b);
+            else atomicOr(&s_grp[g].y, 1u << (b - 32u));
+            // heads before group g = swept packets that start before chunk 64 g.
+            // The packets' chunk ranges tile [0, C) in rank order, so for every
+            // group that starts inside (cstart, cstart + nch] that count is this
+            // packet's rank + 1 (at most 3 groups: nch <= FCAP = 128)
+            for (uint32_t gg = g + 1u; gg < G && (gg << 6) <= cstart + nch[d]; ++gg)
+                s_hb[gg] = (uint16_t)(rank + 1u);
+        }
+        // the next descriptor of this thread follows in rank and chunk order
+        e1 += (big[d] ? 0x10000u : 0u) | (nch[d] ? 1u : 0u);
+        cs += nch[d];
     }
     if (t == 0u) s_hb[0] = 0;
     __syncthreads();
@@ -1017,34 +1043,38 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
     // The sweep summed whole 16-B chunks; subtract, once per packet, the bytes
     // of its first and last chunk that lie outside it (same parity convention,
     // mod 2^32 — exact).
-    uint16_t res = 0;
-    if (i_me < n) {
-        uint32_t acc = s_acc[t];
-        if (meta & (3u << 10)) {
-            const bool odd = meta & (1u << 9);
-            uint32_t c = 0;
-            if (meta & (1u << 10)) {
-                uint4 f = s_edge[2u * t];
-                const int fb1 = (nch == 1u) ? (int)lastv : 16;
-                f.x &= ~byte_range_mask((int)lo, fb1, 0);
-                f.y &= ~byte_range_mask((int)lo, fb1, 1);
-                f.z &= ~byte_range_mask((int)lo, fb1, 2);
-                f.w &= ~byte_range_mask((int)lo, fb1, 3);
-                c += odd ? chunk_words<true>(f) : chunk_words<false>(f);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const uint32_t j = t * D + d, i = tile0 + j;
+        uint16_t res = 0;
+        if (i < n) {
+            uint32_t acc = s_acc[j];
+            if (meta[d] & (3u << 10)) {
+                const bool odd = meta[d] & (1u << 9);
+                uint32_t c = 0;
+                if (meta[d] & (1u << 10)) {
+                    uint4 f = s_edge[2u * j];
+                    const int fb1 = (nch[d] == 1u) ? (int)lastv[d] : 16;
+                    f.x &= ~byte_range_mask((int)lo[d], fb1, 0);
+                    f.y &= ~byte_range_mask((int)lo[d], fb1, 1);
+                    f.z &= ~byte_range_mask((int)lo[d], fb1, 2);
+                    f.w &= ~byte_range_mask((int)lo[d], fb1, 3);
+                    c += odd ? chunk_words<true>(f) : chunk_words<false>(f);
+                }
+                if (meta[d] & (1u << 11)) {
+                    uint4 l = s_edge[2u * j + 1u];
+                    l.x &= ~byte_range_mask(0, (int)lastv[d], 0);
+                    l.y &= ~byte_range_mask(0, (int)lastv[d], 1);
+                    l.z &= ~byte_range_mask(0, (int)lastv[d], 2);
+                    l.w &= ~byte_range_mask(0, (int)lastv[d], 3);
+                    c += odd ? chunk_words<true>(l) : chunk_words<false>(l);
+                }
+                acc -= c;
             }
-            if (meta & (1u << 11)) {
-                uint4 l = s_edge[2u * t + 1u];
-                l.x &= ~byte_range_mask(0, (int)lastv, 0);
-                l.y &= ~byte_range_mask(0, (int)lastv, 1);
-                l.z &= ~byte_range_mask(0, (int)lastv, 2);
-                l.w &= ~byte_range_mask(0, (int)lastv, 3);
-                c += odd ? chunk_words<true>(l) : chunk_words<false>(l);
-            }
-            acc -= c;
+            res = finish(start_sum[d], acc);
         }
-        res = finish(start_sum, acc);
+        src.put(i, res, ctx[d], i < n, a0[d] + lo[d]);
     }
-    src.put(i_me, res, ctx, i_me < n, a0 + lo);
 }
 
 // ------------------------------------------- k_wflat (ragged, window deal) --
@@ -1905,12 +1935,29 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             // 8 KiB in flight per wave; 2-3 % ahead of 4 (8 workgroups, 4 KiB)
             // on mixed in 3 of 4 same-process A/B runs
             if (unroll < 0) unroll = 0;
-            if ((unroll >> 10) != 0) return LVLIP_EINVAL;
+            if ((unroll >> 11) != 0) return LVLIP_EINVAL;
             const int uo = (unroll >> 8) & 3;  // group order + 1 (A/B), 0 = the knob's
+            const bool d2 = (unroll >> 10) & 1;  // 2 descriptors per thread (A/B)
             unroll &= 0xFF;
             if (unroll <= 0) unroll = 8;
             const bool nt = load_nt();
             const int gord = uo ? uo - 1 : flat_group_order();
+            if (d2) {
+                // tiles of 512 descriptors (nontemporal loads only)
+                const uint32_t grid2 = (uint32_t)(((uint64_t)n + 2 * lvlip::FT - 1) / (2 * lvlip::FT));
+                switch (unroll * 8 + gord) {
+#define LVLIP_FLAT_D2(UU, CG)                                                                  \
+    case UU * 8 + CG:                                                                         \
+        hipLaunchKernelGGL((lvlip::k_flat2<UU, true, CG, lvlip::DescSrc, 2>), dim3(grid2),     \
+                           dim3(lvlip::FT), flat_lds_pad(), s, (const uint8_t*)base,         \
+                           lvlip::DescSrc{descs, out}, n);                                  \
+        break;
+                    LVLIP_FLAT_D2(4, 1) LVLIP_FLAT_D2(4, 2) LVLIP_FLAT_D2(8, 1) LVLIP_FLAT_D2(8, 2)
+#undef LVLIP_FLAT_D2
+                    default: return LVLIP_EINVAL;
+                }
+                break;
+            }
             switch (unroll * 8 + (nt ? 4 : 0) + gord) {
 #define LVLIP_FLAT(UU, NTV, CG)                                                               \
     case UU * 8 + (NTV ? 4 : 0) + CG:                                                        \

@@ -43,6 +43,8 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT, 4 | (1 << 8), 0),  # group orders: interleaved, quarters, blocks
     (lvlip.KERNEL_FLAT, 8 | (2 << 8), 0),
     (lvlip.KERNEL_FLAT, 2 | (3 << 8), 0),
+    (lvlip.KERNEL_FLAT, 8 | (1 << 10), 0),            # tiles of 512: 2 descriptors per thread
+    (lvlip.KERNEL_FLAT, 4 | (2 << 8) | (1 << 10), 0),
     (5, 0, 0),                     # first-generation flat kernel (A/B)
     (lvlip.KERNEL_WINDOW, 3, 0),   # interleaved stream: groups dealt round robin
     (lvlip.KERNEL_WINDOW, 2, 1),   # 1 wave/CU: long per-wave sequences, window refills
@@ -228,6 +230,7 @@ def test_full_size_bit_exact(name):
                     (lvlip.KERNEL_WFLAT, 0, 0), (lvlip.KERNEL_WFLAT, 8 | (64 << 8), 16),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
+                    (lvlip.KERNEL_FLAT, 8 | (1 << 10), 0),
                     (lvlip.KERNEL_LANE, 0, 0), (lvlip.KERNEL_AUTO, 0, 0)]:
         assert np.array_equal(run(base, descs, variant, out), want), variant
     # adversarial packets really are there and fold as the reference does
@@ -403,7 +406,9 @@ def test_bad_launch_shapes_rejected():
     base = torch.zeros(64, dtype=torch.uint8, device="cuda")
     descs = dev_descs(mk_descs([0], [4], [0]))
     out = torch.empty(1, dtype=torch.int16, device="cuda")
-    for k, u in ((lvlip.KERNEL_FLAT, 3), (lvlip.KERNEL_FLAT, 8 | (4 << 8)),
+    for k, u in ((lvlip.KERNEL_FLAT, 3), (lvlip.KERNEL_FLAT, 6 | (1 << 10)),
+                 (lvlip.KERNEL_FLAT, 8 | (1 << 8) | (1 << 10)), (lvlip.KERNEL_FLAT, 2 | (1 << 10)),
+                 (lvlip.KERNEL_FLAT, 8 | (1 << 11)),
                  (lvlip.KERNEL_WINDOW, 2 | (5 << 8)), (lvlip.KERNEL_WFLAT, 8 | (48 << 8)),
                  (lvlip.KERNEL_LANE, 3), (lvlip.KERNEL_LANE, 4 | (5 << 8)),
                  (lvlip.KERNEL_LANE, 4 | (1 << 8) | (3 << 16)),
