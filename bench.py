@@ -105,7 +105,12 @@ def traffic_from_profiles(workload: str, kernel_label: str, kernel_fn: str):
                 rec = json.load(f)
         except (OSError, ValueError):
             continue
-        for r in rec.get("kernels", []):
+        kernels = rec.get("kernels") if isinstance(rec, dict) else None
+        if not isinstance(kernels, list):  # other PMC summaries (frames, lane) have other shapes
+            continue
+        for r in kernels:
+            if not isinstance(r, dict):
+                continue
             if (r.get("workload") == workload and r.get("kernel") == kernel_label
                     and r.get("kernel_regex") == kernel_fn):
                 best = r.get("hbm_bytes_per_launch")

@@ -57,6 +57,19 @@ COMMITTED = {
 DOMINANT = {"tcp1500": "k_window", "tcp9000": "k_window", "mixed": "k_flat2"}
 
 
+def test_profile_scan_reads_every_committed_pmc_file():
+    """bench.py takes roofline.traffic from profiles/*pmc*.json: every committed
+    file must parse through that scan (other summaries' shapes included), and
+    the headline workloads find their PMC traffic."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for wl, fn in (("tcp1500", "k_window"), ("tcp9000", "k_window"), ("mixed", "k_flat2")):
+        t = bench.traffic_from_profiles(wl, "auto-u0-w0", fn)
+        assert t is not None and t > 0, wl
+    assert bench.traffic_from_profiles("hdr20", "auto-u0-w0", "k_lane") is None
+
+
 @pytest.mark.parametrize("name", sorted(COMMITTED))
 def test_committed_bench_line_consistent(name):
     algo, max_ratio = COMMITTED[name]
