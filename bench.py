@@ -431,6 +431,8 @@ def frames_dev(lvlip, torch, dev):
     res = {}
     for name, fn, nbytes in (
             ("tx_fill", lambda: lvlip.tx_checksum_dev(base, fdt, stream=stream), 20 * n + l4_bytes),
+            # A/B: the same with plain (temporal) field stores
+            ("tx_fill_plain", lambda: lvlip.tx_checksum_dev(base, fdt, stream=stream), 20 * n + l4_bytes),
             ("rx_header", lambda: lvlip.rx_verify_dev(base, fdt, 0, stream=stream), 20 * n),
             # the header call's A/B kernel (k_flat2 with a frame source)
             ("rx_header_flat", lambda: lvlip.rx_verify_dev(base, fdt, 0, stream=stream), 20 * n),
@@ -438,8 +440,11 @@ def frames_dev(lvlip, torch, dev):
              20 * n + l4_bytes)):
         if name == "rx_header_flat":
             os.environ["LVLIP_FRAMES_RX_HDR"] = "flat"
+        if name == "tx_fill_plain":
+            os.environ["LVLIP_FRAMES_TX_STORE"] = "plain"
         ms = timed(torch, fn, stream, reps=10)
         os.environ.pop("LVLIP_FRAMES_RX_HDR", None)
+        os.environ.pop("LVLIP_FRAMES_TX_STORE", None)
         res[name] = {"ms": round(ms, 4), "Mframes_per_s": round(n / ms / 1e3, 1),
                      "GBps": round(nbytes / ms / 1e6, 1)}
     v = lvlip.rx_verify_dev(base, fdt, 0, stream=stream)

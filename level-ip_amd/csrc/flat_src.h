@@ -149,6 +149,7 @@ struct FrameSrc {
     uint8_t* wbase;                  // the same, writable (TX)
     const lvlip_frame_desc* frames;  // this launch's first frame
     uint8_t* out8;                   // RX: verdict[], TX: status[] (may be null)
+    bool nt_store = false;           // TX: nontemporal field stores (the launcher's default)
     static constexpr uint32_t SLOTS = MODE == FR_RX ? 1u : 2u;
 
     // ip_rcv's decisions (src/ip_input.c:17-60) -> entries {header, L4} and the
@@ -266,7 +267,14 @@ struct FrameSrc {
             // raw store (no htons) of the two bytes; one u16 store when aligned
             const uint64_t fa = addr + (l4 ? (w >> 16) : 10u);
             uint8_t* p = wbase + (fa - reinterpret_cast<uint64_t>(base));
-            if (fa & 1ull) {
+            if (nt_store) {
+                if (fa & 1ull) {
+                    __builtin_nontemporal_store((uint8_t)c, p);
+                    __builtin_nontemporal_store((uint8_t)(c >> 8), p + 1);
+                } else {
+                    __builtin_nontemporal_store(c, reinterpret_cast<uint16_t*>(p));
+                }
+            } else if (fa & 1ull) {
                 p[0] = (uint8_t)c;
                 p[1] = (uint8_t)(c >> 8);
             } else {

@@ -5,8 +5,8 @@ k_rx_hdr and on k_flat2, RX header + L4) the kernel's median duration, HBM bytes
 from the PMC passes, and the algorithmic bytes.
 
 The trace names every flat frame launch `k_flat2` (truncated), so calls are told
-apart by order: bench.py's frames_dev times tx_fill, rx_header (k_rx_hdr),
-rx_header_flat (k_flat2), rx_header_l4, each 3 warm-ups + 10 reps, then one
+apart by order: bench.py's frames_dev times tx_fill (nontemporal field stores),
+tx_fill_plain, rx_header (k_rx_hdr), rx_header_flat (k_flat2), rx_header_l4, each 3 warm-ups + 10 reps, then one
 rx_header for the all-OK check.  That order is checked against the kernel names
 and grid sizes (RX header-only uses one slot per frame, the others two).
 
@@ -27,10 +27,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "level-ip_amd"))
 import workloads  # noqa: E402
 
-MODES = (["tx_fill"] * 13 + ["rx_header"] * 13 + ["rx_header_flat"] * 13 + ["rx_header_l4"] * 13
-         + ["rx_header"])
-KERNEL = {"tx_fill": "k_flat2", "rx_header": "k_rx_hdr", "rx_header_flat": "k_flat2",
-          "rx_header_l4": "k_flat2"}
+MODES = (["tx_fill"] * 13 + ["tx_fill_plain"] * 13 + ["rx_header"] * 13 + ["rx_header_flat"] * 13
+         + ["rx_header_l4"] * 13 + ["rx_header"])
+KERNEL = {"tx_fill": "k_flat2", "tx_fill_plain": "k_flat2", "rx_header": "k_rx_hdr",
+          "rx_header_flat": "k_flat2", "rx_header_l4": "k_flat2"}
 
 
 def dispatches(path, value_col=None):
@@ -45,7 +45,8 @@ def main():
     b = workloads.make("mixed")
     n = b.descs.size // 2
     l4 = int(b.descs[1::2]["len"].sum())
-    algo = {"tx_fill": 20 * n + l4 + 5 * n, "rx_header": 20 * n + n, "rx_header_flat": 20 * n + n,
+    algo = {"tx_fill": 20 * n + l4 + 5 * n, "tx_fill_plain": 20 * n + l4 + 5 * n,
+            "rx_header": 20 * n + n, "rx_header_flat": 20 * n + n,
             "rx_header_l4": 20 * n + l4 + n}
     # the device calls come first; later k_flat2 launches (the host-API timings
     # of bench.py --frames) are not part of this summary

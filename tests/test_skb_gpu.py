@@ -169,6 +169,24 @@ def test_tx_checksum_dev_matches_reference_tx():
     assert np.array_equal(out[mask], buf[mask])
 
 
+def test_tx_checksum_dev_plain_and_nt_stores_agree(monkeypatch):
+    """The device TX fill with both field-store kinds (nontemporal, the default;
+    LVLIP_FRAMES_TX_STORE=plain): identical frames, equal to the oracle's fill,
+    odd and even field addresses (frames at every alignment)."""
+    fr = workloads.frames(3000, seed=58) + workloads.frames(100, seed=59, max_l4=8900)
+    want = [bytearray(f) for f in fr]
+    for f in want:
+        skb_oracle.tx_fill(f)
+    buf, fd = lvlip.pack_frames(fr, align_mod=16, seed=5)
+    for kind in ("nt", "plain"):
+        monkeypatch.setenv("LVLIP_FRAMES_TX_STORE", kind)
+        base = _dev(buf)
+        assert int(lvlip.tx_checksum_dev(base, fd).sum()) == len(fr), kind
+        out = base.cpu().numpy()
+        got = [out[int(d["offset"]):int(d["offset"]) + int(d["len"])].tobytes() for d in fd]
+        assert got == [bytes(f) for f in want], kind
+
+
 def test_tx_dev_then_rx_dev_roundtrip_large():
     """2^17 frames built and filled on the GPU verify OK on the GPU (header and,
     where the TCP seed kept its carry, L4), matching the host path verdicts."""
