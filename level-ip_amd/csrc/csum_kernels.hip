@@ -1471,12 +1471,13 @@ __global__ __launch_bounds__(256) void k_lane(const uint8_t* __restrict__ base,
 // --------------------------------------------- k_rx_hdr (RX header verify) --
 //
 // f1's header-only RX call (lvlip_rx_verify_dev without LVLIP_RX_VERIFY_L4) as
-// one lane per frame.  The parse window FrWin already holds frame bytes
-// [12, 56): the whole IPv4 header for ihl <= 10, so the lane sums it from
-// registers (header dword m = window bytes 14+4m .. 17+4m, one alignbyte each)
-// and no entry, tile plan or second read of the header exists.  Headers with
-// more options (ihl 11-15) read their last words with byte loads.  The
-// decisions are FrameSrc<FR_RX>'s (parse_rx) and the verdict rule its put's.
+// one lane per frame.  The parse window FrWin, here its first three chunks,
+// holds frame bytes [12, 45) at least: the whole IPv4 header for ihl 5-7, so
+// the lane sums it from registers (header dword m = window bytes 14+4m ..
+// 17+4m, one alignbyte each) and no entry, tile plan or second read of the
+// header exists.  Header words past the window (options) come from byte
+// loads.  The decisions are FrameSrc<FR_RX>'s (parse_rx) and the verdict
+// rule its put's.
 __global__ __launch_bounds__(256) void k_rx_hdr(const uint8_t* __restrict__ base,
                                                 const lvlip_frame_desc* __restrict__ frames,
                                                 uint32_t n, uint8_t* __restrict__ verdict) {
@@ -1489,8 +1490,11 @@ __global__ __launch_bounds__(256) void k_rx_hdr(const uint8_t* __restrict__ base
     fd.len = raw.z;
     fd.reserved = 0;
     const uint8_t* h = base + fd.offset;
+    // three chunks: frame bytes [12, cov), cov >= 45 (FrWin::load<3>), which
+    // hold every field parse_rx reads in this mode and the header of ihl 5-7
     FrWin x;
-    x.load(h, fd.len, reinterpret_cast<uint64_t>(frames + f) & ~15ull);
+    x.load<3>(h, fd.len, reinterpret_cast<uint64_t>(frames + f) & ~15ull);
+    const uint32_t cov = 60u - (uint32_t)((reinterpret_cast<uint64_t>(h) + 12u) & 15u);
     lvlip_csum_desc d0 = fr_mk(0, 0, 0), d1 = fr_mk(0, 0, 0);
     uint32_t w = 0;
     src.parse_rx(fd, x, d0, d1, w);
@@ -1499,8 +1503,14 @@ __global__ __launch_bounds__(256) void k_rx_hdr(const uint8_t* __restrict__ base
         const uint32_t ihl = x.b(14) & 0x0fu;
         uint32_t acc = 0;
 #pragma unroll
-        for (uint32_t m = 0; m < 10u; ++m)
-            acc = dot2_acc(m < ihl ? __builtin_amdgcn_alignbyte(x.A[m + 1u], x.A[m], 2u) : 0u, acc);
+        for (uint32_t m = 0; m < 10u; ++m) {
+            // header dword m = frame bytes 14+4m .. 17+4m: from the window when
+            // it holds them, else from memory (options past the window)
+            const bool inw = 18u + 4u * m <= cov;
+            uint32_t hd = __builtin_amdgcn_alignbyte(x.A[m + 1u], x.A[m], 2u);
+            if (m < ihl && !inw) hd = fr_le16(h + 14u + 4u * m) | (fr_le16(h + 16u + 4u * m) << 16);
+            acc = dot2_acc(m < ihl ? hd : 0u, acc);
+        }
         for (uint32_t k = 54u; k < FR_ETH + 4u * ihl; k += 2u) acc += fr_le16(h + k);
         // src/ip_input.c:38-43, as FrameSrc<FR_RX>::put
         if (finish(0u, acc) != 0u) v = LVLIP_RX_BAD_CSUM;

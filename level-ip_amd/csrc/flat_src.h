@@ -84,7 +84,11 @@ __device__ __forceinline__ lvlip_csum_desc fr_mk(uint64_t off, uint32_t len, uin
 struct FrWin {
     uint32_t A[11];
     // safe: a readable 16-B aligned address for a frame with no byte in the
-    // window (a chunk of the frame's own descriptor)
+    // window (a chunk of the frame's own descriptor).  NCH = 3 loads only the
+    // first three chunks (frame bytes [12, cov) with cov = 60 - ((h + 12) & 15)
+    // >= 45 are then valid; the header-only RX kernel, which reads no field
+    // past byte 23 and sums the header words past cov from memory).
+    template <int NCH = 4>
     __device__ __forceinline__ void load(const uint8_t* h, uint32_t len, uint64_t safe) {
         const uint64_t p = reinterpret_cast<uint64_t>(h) + 12u;
         const uint64_t a = p & ~15ull, end = reinterpret_cast<uint64_t>(h) + len;
@@ -98,19 +102,31 @@ struct FrWin {
         uint64_t ad[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) ad[k] = a + 16u * k < end ? a + 16u * k : a0;
-        asm volatile(
-            "global_load_dwordx4 %0, %4, off\n\t"
-            "global_load_dwordx4 %1, %5, off\n\t"
-            "global_load_dwordx4 %2, %6, off\n\t"
-            "global_load_dwordx4 %3, %7, off\n\t"
-            "s_waitcnt vmcnt(0)"
-            : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3])
-            : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
-            : "memory");
+        if (NCH == 4) {
+            asm volatile(
+                "global_load_dwordx4 %0, %4, off\n\t"
+                "global_load_dwordx4 %1, %5, off\n\t"
+                "global_load_dwordx4 %2, %6, off\n\t"
+                "global_load_dwordx4 %3, %7, off\n\t"
+                "s_waitcnt vmcnt(0)"
+                : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3])
+                : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
+                : "memory");
+        } else {
+            asm volatile(
+                "global_load_dwordx4 %0, %3, off\n\t"
+                "global_load_dwordx4 %1, %4, off\n\t"
+                "global_load_dwordx4 %2, %5, off\n\t"
+                "s_waitcnt vmcnt(0)"
+                : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2])
+                : "v"(ad[0]), "v"(ad[1]), "v"(ad[2])
+                : "memory");
+            c[3] = v4u{0u, 0u, 0u, 0u};
+        }
         uint32_t W[16];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t m = a + 16u * k < end ? 0xffffffffu : 0u;
+            const uint32_t m = (k < NCH && a + 16u * k < end) ? 0xffffffffu : 0u;
             W[4 * k] = c[k].x & m;
             W[4 * k + 1] = c[k].y & m;
             W[4 * k + 2] = c[k].z & m;
