@@ -474,6 +474,35 @@ def test_host_direct_and_copied_pieces(monkeypatch, direct_max):
         assert np.array_equal(ctx.batch_host_flat(buf, b.descs), want)
 
 
+@pytest.mark.parametrize("direct_max", ["0", "1000000000000"])
+def test_host_tiny_packets_lane_path(monkeypatch, direct_max):
+    """Host batches of IPv4-header-sized packets (0-32 B at any address): the
+    gathered pieces' average slot is <= 32 B, so AUTO runs k_lane on them, read
+    in the pinned arena (direct) or after the copy engine; a few 1-9 KB packets
+    among them take its whole-wave loop.  Against the oracle."""
+    monkeypatch.setenv("LVLIP_DIRECT_MAX", direct_max)
+    rng = np.random.default_rng(17)
+    pool = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    pkts, starts, want = [], [], []
+    for i in range(30000):
+        ln = int(rng.integers(0, 33)) if i % 997 else int(rng.integers(1000, 9000))
+        off = int(rng.integers(0, pool.size - ln))
+        pkts.append(pool[off:off + ln])
+        st = int(rng.integers(0, 2**32))
+        starts.append(st)
+        want.append(pyoracle.checksum(pool[off:off + max(ln, 1)], ln, st))
+    with lvlip.Context(0, arena_bytes=256 << 10) as ctx:
+        assert list(ctx.batch_host(pkts, starts)) == want
+    # IPv4 headers at skb offset 14 of 64-B frames, flat in one host buffer
+    n = 20000
+    frames = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+    d = mk_descs(np.arange(n, dtype=np.uint64) * 64 + 14, np.full(n, 20, np.int32),
+                 np.zeros(n, dtype=np.uint32))
+    host = frames.reshape(-1)
+    with lvlip.Context(0) as ctx:
+        assert np.array_equal(ctx.batch_host_flat(host, d), pyoracle.batch(host, d))
+
+
 def test_lab_read_probe_sums():
     lab = lvlip.lab()
     a = torch.arange(0, 1 << 20, dtype=torch.int32, device="cuda")
