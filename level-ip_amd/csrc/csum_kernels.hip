@@ -857,36 +857,72 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
 
     // ---- phase 1: descriptors -> chunk counts, ranks, records, head bitmap
     uint32_t start_sum[D], nch[D], meta[D], lo[D], lastv[D], ctx[D];
-    uint64_t a0[D];  // the entry's first byte is a0 + lo
+    uint64_t a0[D];  // the swept part's first chunk; its first byte is a0 + lo
+    uint64_t ent[D];  // the entry's first byte (the frame calls' put)
     bool big[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const uint32_t j = t * D + d, i = tile0 + j;
         start_sum[d] = 0, nch[d] = 0, meta[d] = 0, lo[d] = 0, lastv[d] = 16, ctx[d] = 0;
         a0[d] = 0;
+        ent[d] = 0;
         big[d] = false;
+        uint32_t wsum = 0;  // the entry's bytes inside the parse window (frame calls)
         if (i < n) {
-            const lvlip_csum_desc ds = src.get(i, ctx[d]);
+            uint4 win[4];
+            uint64_t wa = 0;
+            lvlip_csum_desc ds;
+            if constexpr (Src::WIN_SUM)
+                ds = src.get(i, ctx[d], win, &wa);
+            else
+                ds = src.get(i, ctx[d]);
             start_sum[d] = ds.start_sum;
             if (ds.len > 0) {
-                const uint64_t abs = reinterpret_cast<uint64_t>(base) + ds.offset;
-                a0[d] = abs & ~15ull;
-                lo[d] = (uint32_t)(abs & 15ull);
-                const uint64_t span = (uint64_t)lo[d] + (uint64_t)(uint32_t)ds.len;
-                const uint64_t c64 = (span + 15u) >> 4;
-                lastv[d] = (uint32_t)(span - 16ull * (c64 - 1u));
+                uint64_t abs = reinterpret_cast<uint64_t>(base) + ds.offset;
+                const uint64_t eend = abs + (uint32_t)ds.len;
+                ent[d] = abs;
                 const bool odd = abs & 1ull;
-                big[d] = c64 > FCAP;
-                nch[d] = big[d] ? 0u : (uint32_t)c64;
-                // edge flags: the sweep stashes the packet's first (bit 10) and
-                // last (bit 11) chunk in LDS when they hold bytes outside it
-                const bool ef = !big[d] && (lo[d] != 0u || (c64 == 1u && lastv[d] != 16u));
-                const bool el = !big[d] && c64 > 1u && lastv[d] != 16u;
-                meta[d] = nch[d] | ((uint32_t)odd << 9) | ((uint32_t)ef << 10) | ((uint32_t)el << 11) |
-                          (j << 18);
+                big[d] = (((abs & 15ull) + (uint32_t)ds.len + 15u) >> 4) > FCAP;
+                if constexpr (Src::WIN_SUM) {
+                    // Frame calls: the parse already holds the frame's chunks
+                    // [wa, wa + 64) in registers.  Sum the entry's bytes there
+                    // (same masking and parity as the sweep plus the edge
+                    // corrections) and sweep only the rest, from wa + 64: the
+                    // header entry then needs no sweep at all, and no frame
+                    // byte is read from HBM twice.  Big entries keep the
+                    // whole-wave loop over all their bytes.
+                    const uint64_t we = wa + 64u;
+                    if (!big[d] && abs >= wa && abs < we) {
+                        const uint64_t pe = eend < we ? eend : we;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const uint64_t ck = wa + 16u * k;
+                            const int b0 = abs > ck ? (int)(abs - ck < 16u ? abs - ck : 16u) : 0;
+                            const int b1 = pe > ck ? (int)(pe - ck < 16u ? pe - ck : 16u) : 0;
+                            const uint4 v = mask_chunk(win[k], b0, b1);
+                            wsum += odd ? chunk_words<true>(v) : chunk_words<false>(v);
+                        }
+                        abs = pe;
+                    }
+                }
+                if (abs < eend) {
+                    a0[d] = abs & ~15ull;
+                    lo[d] = (uint32_t)(abs & 15ull);
+                    const uint64_t span = (uint64_t)lo[d] + (eend - abs);
+                    const uint64_t c64 = (span + 15u) >> 4;
+                    lastv[d] = (uint32_t)(span - 16ull * (c64 - 1u));
+                    nch[d] = big[d] ? 0u : (uint32_t)c64;
+                    // edge flags: the sweep stashes the packet's first (bit 10)
+                    // and last (bit 11) chunk in LDS when they hold bytes
+                    // outside it
+                    const bool ef = !big[d] && (lo[d] != 0u || (c64 == 1u && lastv[d] != 16u));
+                    const bool el = !big[d] && c64 > 1u && lastv[d] != 16u;
+                    meta[d] = nch[d] | ((uint32_t)odd << 9) | ((uint32_t)ef << 10) |
+                              ((uint32_t)el << 11) | (j << 18);
+                }
             }
         }
-        s_acc[j] = 0u;
+        s_acc[j] = wsum;
     }
     for (uint32_t g = t; g < FG; g += FT) s_grp[g] = make_uint2(0u, 0u);
     // one scan pass for three prefixes: big packets (high half) and swept
@@ -1073,7 +1109,7 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
             }
             res = finish(start_sum[d], acc);
         }
-        src.put(i, res, ctx[d], i < n, a0[d] + lo[d]);
+        src.put(i, res, ctx[d], i < n, ent[d]);
     }
 }
 

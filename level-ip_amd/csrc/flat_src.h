@@ -20,6 +20,7 @@
 namespace lvlip {
 
 struct DescSrc {
+    static constexpr bool WIN_SUM = false;  // no parse window (see FrameSrc)
     const lvlip_csum_desc* descs;
     uint16_t* out;
     // One 16-B load: read field by field, hipcc splits the descriptor into a
@@ -83,6 +84,8 @@ __device__ __forceinline__ lvlip_csum_desc fr_mk(uint64_t off, uint32_t len, uin
 // frame's len read as whatever the chunk holds and are never used.
 struct FrWin {
     uint32_t A[11];
+    uint4 raw[4];     // the window's chunks as loaded (zero past the frame's end)
+    uint64_t abase;   // address of raw[0]
     // safe: a readable 16-B aligned address for a frame with no byte in the
     // window (a chunk of the frame's own descriptor).  NCH = 3 loads only the
     // first three chunks (frame bytes [12, cov) with cov = 60 - ((h + 12) & 15)
@@ -131,7 +134,9 @@ struct FrWin {
             W[4 * k + 1] = c[k].y & m;
             W[4 * k + 2] = c[k].z & m;
             W[4 * k + 3] = c[k].w & m;
+            raw[k] = make_uint4(W[4 * k], W[4 * k + 1], W[4 * k + 2], W[4 * k + 3]);
         }
+        abase = a;
         // L[j] = W[j + q] by bit selects (no divergent branch), then one
         // alignbyte per output dword
         const uint32_t q = (uint32_t)(p & 15u) >> 2, r = (uint32_t)p & 3u;
@@ -167,6 +172,10 @@ struct FrameSrc {
     uint8_t* out8;                   // RX: verdict[], TX: status[] (may be null)
     bool nt_store = false;           // TX: nontemporal field stores (the launcher's default)
     static constexpr uint32_t SLOTS = MODE == FR_RX ? 1u : 2u;
+    // The parse window's chunks are in registers after get(): k_flat2 sums
+    // each entry's bytes inside the window there and sweeps only the rest, so
+    // no frame byte is read from HBM twice.
+    static constexpr bool WIN_SUM = true;
 
     // ip_rcv's decisions (src/ip_input.c:17-60) -> entries {header, L4} and the
     // plan word (verdict so far | flags)
@@ -236,7 +245,8 @@ struct FrameSrc {
         w |= 1u;
     }
 
-    __device__ __forceinline__ lvlip_csum_desc get(uint32_t i, uint32_t& w) const {
+    __device__ __forceinline__ lvlip_csum_desc get(uint32_t i, uint32_t& w, uint4* win = nullptr,
+                                                   uint64_t* wa = nullptr) const {
         // the descriptor's two words in flight together (the compiler would
         // load len, branch on it, then load offset)
         typedef uint32_t v2u __attribute__((ext_vector_type(2)));
@@ -261,6 +271,11 @@ struct FrameSrc {
             parse_tx(fd, h, x, d0, d1, w);
         else
             parse_rx(fd, x, d0, d1, w);
+        if (win) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) win[k] = x.raw[k];
+            *wa = x.abase;
+        }
         return (SLOTS == 2u && (i & 1u)) ? d1 : d0;
     }
 
