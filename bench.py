@@ -438,13 +438,21 @@ def frames_dev(lvlip, torch, dev):
             ("rx_header_flat", lambda: lvlip.rx_verify_dev(base, fdt, 0, stream=stream), 20 * n),
             ("rx_header_l4", lambda: lvlip.rx_verify_dev(base, fdt, lvlip.RX_VERIFY_L4, stream=stream),
              20 * n + l4_bytes)):
-        if name == "rx_header_flat":
-            os.environ["LVLIP_FRAMES_RX_HDR"] = "flat"
-        if name == "tx_fill_plain":
-            os.environ["LVLIP_FRAMES_TX_STORE"] = "plain"
-        ms = timed(torch, fn, stream, reps=10)
-        os.environ.pop("LVLIP_FRAMES_RX_HDR", None)
-        os.environ.pop("LVLIP_FRAMES_TX_STORE", None)
+        # the A/B kernels are selected by knobs the library reads per call;
+        # the caller's own settings come back afterwards
+        knob = {"rx_header_flat": ("LVLIP_FRAMES_RX_HDR", "flat"),
+                "tx_fill_plain": ("LVLIP_FRAMES_TX_STORE", "plain")}.get(name)
+        saved = os.environ.get(knob[0]) if knob else None
+        if knob:
+            os.environ[knob[0]] = knob[1]
+        try:
+            ms = timed(torch, fn, stream, reps=10)
+        finally:
+            if knob:
+                if saved is None:
+                    os.environ.pop(knob[0], None)
+                else:
+                    os.environ[knob[0]] = saved
         res[name] = {"ms": round(ms, 4), "Mframes_per_s": round(n / ms / 1e3, 1),
                      "GBps": round(nbytes / ms / 1e6, 1)}
     v = lvlip.rx_verify_dev(base, fdt, 0, stream=stream)
