@@ -7,31 +7,42 @@ segments).  Prints ONE JSON line (rank 0):
 
   value       whole-job GB/s = sum over ranks of algorithmic bytes x K / max-over-ranks time
   roofline    the checksum kernel's achieved algorithmic GB/s (HIP events on the launch
-              stream) against the 8 TB/s HBM3E peak; traffic = PMC-measured HBM bytes per
-              launch from profiles/ when a matching measurement is committed, else null
-  cpu_baseline  the reference's own checksum() (oracle/_ref, -O0 as its Makefile builds
-              it) on the host cores, over a bounded sample of the same packets (rank 0, N=1)
+              stream) against the 8 TB/s HBM3E peak; frac_aggregate = value / (N x 8 TB/s);
+              traffic = PMC-measured HBM bytes per launch from profiles/ when a matching
+              measurement is committed, else null
+  verified_bit_exact  every one of the N outputs of the timed batch, copied back from
+              HBM after the timed loop, equals level-ip's own checksum() (oracle/_ref,
+              compiled from src/utils.c) run over the same bytes; on every rank
+  cpu_baseline  that reference checksum() on the host cores (rank 0, N=1): all
+              cores of the process's affinity mask over the whole timed batch, plus
+              one-core and 16-thread figures
 
 Before the W warm-up steps every rank runs untimed steps for --settle-ms of wall
 time (default 250 ms), so the timed region starts at the GPU's sustained clocks
 rather than in its ramp from idle (diag.settle).
 
-Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`;
-each rank checksums its own shard (packets rank*n .. rank*n+n-1 of the stream:
-weak scaling, no collective on the data path); RCCL is used only for the
-barriers and the max-over-ranks time.
+Multi-GPU (BASELINE configs[4]): `python bench.py --gpus N` starts
+its N ranks itself, one process per GPU, before anything in the parent touches
+the GPU; under `python -m torch.distributed.run --nproc-per-node N bench.py --gpus
+N` the launcher's ranks are used instead (WORLD_SIZE must equal N).  Every rank
+checksums its own shard (packets rank*n .. rank*n+n-1 of the stream: weak
+scaling, no collective on the data path); RCCL carries only the barriers, the
+max-over-ranks time and the per-rank report.  Under RCCL every rank must own a
+distinct GPU (checked by PCI bus id); LVLIP_DIST_BACKEND=gloo rehearses several
+ranks on one GPU.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "level-ip_amd"))
-sys.path.insert(0, os.path.join(ROOT, "oracle"))  # cpu_baseline leg only (pyoracle)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))  # checker + cpu_baseline leg only (pyoracle)
 
 import numpy as np  # noqa: E402
 
@@ -48,11 +59,14 @@ WORKLOAD_TEXT = {
                    "16-B aligned slots (stride 1504)",
 }
 STRONG = {"tcp1500x64m": 64 << 20}  # workload -> total packets over all ranks
+VERIFY_SPAN = 2 << 30  # host bytes per verification chunk (copied back from HBM)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs = ranks on this node (default: WORLD_SIZE, else 1).  N > 1 "
+                        "without a torch.distributed launcher: bench.py starts the N ranks")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--settle-ms", type=float, default=250.0,
@@ -69,6 +83,9 @@ def parse():
     p.add_argument("--waves-per-cu", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--dry-run", action="store_true",
+                   help="rehearse the launch / rendezvous / report path on the CPU (gloo, no "
+                        "GPU work, small batch): the line carries dry_run=true and no throughput")
     p.add_argument("--sweep", action="store_true", help="also time every kernel variant (stderr)")
     p.add_argument("--frames", action="store_true",
                    help="diag: device-resident frame batches (TX fill, RX verify) on the mixed frames")
@@ -77,7 +94,7 @@ def parse():
                         "point to point first (timed separately, diag.scatter)")
     p.add_argument("--e2e", action="store_true",
                    help="also time the host-resident path (PCIe-inclusive; stderr + diag)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def log(*a):
@@ -117,66 +134,23 @@ def traffic_from_profiles(workload: str, kernel_label: str, kernel_fn: str):
     return best
 
 
-def cpu_baseline(b, threads: int, kernel: int, unroll: int, wpc: int, dev, len_hint: int = 0,
-                 budget_s: float = 1.0):
-    """Reference checksum() over a bounded sample of the same workload on the host.
+# ------------------------------------------------------------------ host CPUs --
 
-    The same sample also goes through the GPU kernel being benchmarked and is
-    compared bit for bit with the reference's outputs (verified_bit_exact)."""
-    import pyoracle  # test infrastructure: the reported CPU baseline / checker only
-    import torch
-
-    import lvlip
-    import workloads
-
-    sample_pkts = min(b.n, 131072)
-    sb = workloads.make(b.name, n=sample_pkts // (2 if b.name == "mixed" else 1))
-    host = sb.host_bytes()
-    use_ref = pyoracle.reflib() is not None
-    kind = "reference" if use_ref else "port"
-    ref_out = pyoracle.batch(host, sb.descs, threads=threads, opt=0, use_reference=use_ref)
-    sbase, sdescs, sout = workloads.to_device(sb, dev)
-    lvlip.batch_dev(sbase.data_ptr(), sdescs.data_ptr(), sb.n, sout.data_ptr(),
-                    torch.cuda.current_stream(dev).cuda_stream, kernel, unroll, wpc, len_hint)
-    torch.cuda.synchronize(dev)
-    verified = bool(np.array_equal(sout.cpu().numpy().view(np.uint16), ref_out))
-    if not verified:
-        raise SystemExit("GPU checksums differ from the reference on the baseline sample")
-    out = {}
-    for label, thr in (("all", threads), ("one", 1)):
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            pyoracle.batch(host, sb.descs, threads=thr, opt=0, use_reference=use_ref)
-            reps += 1
-            dt = time.perf_counter() - t0
-            if dt >= (budget_s if thr > 1 else budget_s * 2):
-                break
-        out[label] = (sb.algo_bytes * reps / dt / 1e9, reps, dt)
-    # the product's own per-call drop-in (Group 1, CPU) through the same harness
-    t0 = time.perf_counter()
-    reps1 = 0
-    while time.perf_counter() - t0 < budget_s:
-        pyoracle.batch(host, sb.descs, threads=1, csum_fn=lvlip.lib().checksum)
-        reps1 += 1
-    dropin = sb.algo_bytes * reps1 / (time.perf_counter() - t0) / 1e9
-    # the same algorithm (oracle restatement of src/utils.c:22-55) at -O2, one core
-    t0 = time.perf_counter()
-    reps2 = 0
-    while time.perf_counter() - t0 < budget_s:
-        pyoracle.batch(host, sb.descs, threads=1, opt=2)
-        reps2 += 1
-    o2 = sb.algo_bytes * reps2 / (time.perf_counter() - t0) / 1e9
-    gbps, reps, dt = out["all"]
-    return {
-        "value": round(gbps, 3), "unit": "GB/s", "cores": threads, "kind": kind,
-        "sample": (f"{sb.n} descriptors / {sb.algo_bytes / 1e6:.1f} MB of the {b.name} workload, "
-                   f"{reps} passes in {dt:.2f} s on {threads} threads (pthreads over contiguous "
-                   f"packet ranges); level-ip {'src/utils.c compiled -O0 as its Makefile builds it' if use_ref else 'oracle restatement -O0'}"),
-        "one_core_GBps": round(out["one"][0], 3),
-        "one_core_O2_restatement_GBps": round(o2, 3),
-        "dropin_one_core_GBps": round(dropin, 3),
-        "cpu_model": _cpu_model(),
-    }, verified
+def host_cpus() -> dict:
+    """What the host offers this process: the affinity mask (what threads can
+    run on), os.cpu_count() (the machine) and the cgroup CPU quota, if any."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+        except (OSError, ValueError):
+            pass
+    return {"nproc": aff, "machine_cpus": os.cpu_count(), "cgroup_cpu_quota": quota,
+            "cpu_model": _cpu_model()}
 
 
 def _cpu_model():
@@ -190,32 +164,220 @@ def _cpu_model():
     return "unknown"
 
 
-def main():
-    args = parse()
+# ------------------------------------------------------------- verification --
+
+def _chunks(descs: np.ndarray, span_max: int):
+    """Consecutive descriptor ranges [lo, hi) whose byte span is at most
+    span_max (a single descriptor may exceed it), with the span's start."""
+    n = descs.size
+    off = descs["offset"].astype(np.uint64)
+    end = off + np.maximum(descs["len"], 0).astype(np.uint64)
+    lo = 0
+    step = max(1, n)
+    while lo < n:
+        hi = min(n, lo + step)
+        while True:
+            a = int(off[lo:hi].min()) & ~15
+            e = int(end[lo:hi].max())
+            if e - a <= span_max or hi - lo == 1:
+                break
+            hi = lo + max(1, (hi - lo) // 2)
+        step = max(hi - lo, 1)
+        yield lo, hi, a, (e + 15) & ~15
+        lo = hi
+
+
+def verify_timed_batch(b, base, out, threads: int, keep_first: bool):
+    """All outputs of the timed batch against level-ip's own checksum() over the
+    same bytes, copied back from HBM after the timed loop (the checker: oracle/_ref,
+    or the oracle restatement where the reference was not built).
+
+    Returns (result dict, (host bytes, rebased descriptors) of the first chunk
+    when keep_first, for the CPU baseline)."""
+    import pyoracle  # test infrastructure: the checker
+
+    use_ref = pyoracle.reflib() is not None
+    got_all = out[: b.n].cpu().numpy().view(np.uint16)
+    bad, ref_s, first = 0, 0.0, None
+    for lo, hi, a, e in _chunks(b.descs, VERIFY_SPAN):
+        host = base[a:e].cpu().numpy()
+        d = b.descs[lo:hi].copy()
+        d["offset"] -= np.uint64(a)
+        t0 = time.perf_counter()
+        want = pyoracle.batch(host, d, threads=threads, opt=0, use_reference=use_ref)
+        ref_s += time.perf_counter() - t0
+        bad += int(np.count_nonzero(want != got_all[lo:hi]))
+        if keep_first and first is None:
+            first = (host, d)
+    return {"ok": bad == 0, "descriptors": b.n, "mismatches": bad,
+            "checker": "reference" if use_ref else "port", "threads": threads,
+            "checker_s": round(ref_s, 3)}, first
+
+
+def cpu_baseline(b, first, cpus: dict, budget_s: float = 1.0):
+    """level-ip's checksum() (oracle/_ref, -O0 as its Makefile builds it) on the
+    host: every core of the affinity mask over the timed batch's bytes (its
+    first <= 2 GiB, the whole batch for configs[1]), pthreads over contiguous
+    packet ranges; plus 16 threads, one core, the same algorithm at -O2 and the
+    product's own per-call drop-in on a 131 072-descriptor sample."""
+    import pyoracle  # test infrastructure: the reported CPU baseline only
+
+    import lvlip
+
+    use_ref = pyoracle.reflib() is not None
+    kind = "reference" if use_ref else "port"
+    host, d = first
+    nbytes = int(np.maximum(d["len"], 0).sum()) + 2 * d.size
+
+    def rate(h, dd, thr, nb, budget, **kw):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            pyoracle.batch(h, dd, threads=thr, **kw)
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget:
+                return nb * reps / dt / 1e9, reps, dt
+
+    cores = cpus["nproc"]
+    allc, reps, dt = rate(host, d, cores, nbytes, budget_s, opt=0, use_reference=use_ref)
+    t16 = min(16, cores)
+    g16 = rate(host, d, t16, nbytes, budget_s, opt=0, use_reference=use_ref)[0]
+    # one-core figures on a sample (the same packets' first descriptors)
+    ns = min(d.size, 131072)
+    sd = d[:ns].copy()
+    ea = int((sd["offset"] + np.maximum(sd["len"], 0).astype(np.uint64)).max())
+    sh = host[: (ea + 15) & ~15]
+    sb = int(np.maximum(sd["len"], 0).sum()) + 2 * ns
+    one = rate(sh, sd, 1, sb, 2 * budget_s, opt=0, use_reference=use_ref)[0]
+    o2 = rate(sh, sd, 1, sb, budget_s, opt=2)[0]
+    dropin = rate(sh, sd, 1, sb, budget_s, csum_fn=lvlip.lib().checksum)[0]
+    return {
+        "value": round(allc, 3), "unit": "GB/s", "cores": cores, "kind": kind,
+        "sample": (f"{d.size} descriptors / {nbytes / 1e6:.1f} MB of the timed {b.name} batch, "
+                   f"copied back from HBM; {reps} passes in {dt:.2f} s on {cores} threads "
+                   f"(pthreads over contiguous packet ranges, every CPU of the affinity mask); "
+                   f"level-ip {'src/utils.c compiled -O0 as its Makefile builds it' if use_ref else 'oracle restatement -O0'}"),
+        "nproc": cpus["nproc"], "cores_used": cores, "machine_cpus": cpus["machine_cpus"],
+        "cgroup_cpu_quota": cpus["cgroup_cpu_quota"], "cpu_model": cpus["cpu_model"],
+        "threads16_GBps": round(g16, 3),
+        "one_core_GBps": round(one, 3),
+        "one_core_O2_restatement_GBps": round(o2, 3),
+        "dropin_one_core_GBps": round(dropin, 3),
+    }
+
+
+# ------------------------------------------------------------------ launcher --
+
+def self_launch(world: int) -> int:
+    """`bench.py --gpus N` without a torch.distributed launcher: start the N
+    ranks as child processes of this one (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* as torch.distributed.run sets them), one GPU each.  This process
+    never touches the GPU (no torch import).  If a rank fails, the others are
+    stopped (by PID) and the first failure's status is returned."""
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
+                   LOCAL_WORLD_SIZE=str(world), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), LVLIP_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc, live = 0, list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 1
+                log(f"bench.py: rank {procs.index(p)} exited with status {r}; stopping the others")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.02)
+    return rc
+
+
+def main(argv=None):
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        world = args.gpus if args.gpus is not None else 1
+        if world < 1:
+            raise SystemExit("bench.py: --gpus must be >= 1")
+        if world > 1:
+            raise SystemExit(self_launch(world))
+    else:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} "
+                             "ranks; they must agree")
+    run(args, world)
+
+
+def _rank_info(torch, dev, rank: int, local: int) -> dict:
+    info = {"rank": rank, "local_rank": local, "host": socket.gethostname()}
+    if dev is not None and dev.type == "cuda":
+        p = torch.cuda.get_device_properties(dev)
+        info.update({"device": dev.index, "name": p.name,
+                     "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+                     "uuid": str(getattr(p, "uuid", ""))})
+    return info
+
+
+def run(args, world: int):
     import torch
     import torch.distributed as dist
 
-    import lvlip
     import workloads
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # RCCL (backend "nccl") on the 8-GPU node; LVLIP_DIST_BACKEND=gloo rehearses the
-    # N>1 code path with several ranks on one GPU (device = local rank mod count).
-    backend = os.environ.get("LVLIP_DIST_BACKEND", "nccl")
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(dev)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-    coll_dev = dev if backend == "nccl" else torch.device("cpu")
-    if lvlip.device_count() == 0:
-        raise SystemExit("bench.py needs a HIP device")
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    launcher = os.environ.get("LVLIP_BENCH_LAUNCHER") or ("torch.distributed.run" if world > 1 else None)
+    # RCCL (backend "nccl") across the node's GPUs, one per rank;
+    # LVLIP_DIST_BACKEND=gloo rehearses the N>1 code path with several ranks on
+    # one GPU (device = local rank mod count); --dry-run has no GPU at all.
+    backend = "gloo" if args.dry_run else os.environ.get("LVLIP_DIST_BACKEND", "nccl")
+    dev = None
+    if not args.dry_run:
+        import lvlip
 
-    kernel = lvlip.KERNEL_NAMES[args.kernel]
+        ndev = torch.cuda.device_count()
+        if ndev == 0 or lvlip.device_count() == 0:
+            raise SystemExit(f"bench.py rank {rank}: needs a HIP device (none visible)")
+        if backend == "nccl" and world > 1:
+            if ndev < local_world:
+                raise SystemExit(
+                    f"bench.py rank {rank}: {local_world} ranks on this node need {local_world} GPUs "
+                    f"(one per rank under RCCL), {ndev} visible; LVLIP_DIST_BACKEND=gloo rehearses "
+                    "several ranks on one GPU")
+            dev = torch.device("cuda", local)
+        else:
+            dev = torch.device("cuda", local % ndev)
+        torch.cuda.set_device(dev)
+    if world > 1:
+        from datetime import timedelta
+
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, timeout=timedelta(minutes=10))
+        else:
+            dist.init_process_group(backend, timeout=timedelta(minutes=10))
+    coll_dev = dev if backend == "nccl" and world > 1 else torch.device("cpu")
+
+    ranks = [_rank_info(torch, dev, rank, local)]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, _rank_info(torch, dev, rank, local))
+        if backend == "nccl":
+            where = [(r["host"], r.get("pci")) for r in ranks]
+            if len(set(where)) != world:
+                raise SystemExit(f"bench.py rank {rank}: ranks share a GPU under RCCL: {where}")
+
     if args.workload in STRONG:
         # strong scaling: a fixed batch, contiguous packet ranges per rank
         total = args.n or STRONG[args.workload]
@@ -225,8 +387,11 @@ def main():
         # weak scaling: each rank owns the next n packets of the stream
         n = args.n or (1 << 21 if args.workload == "mixed" else 1 << 20)
         first = rank * n
+    if args.dry_run:
+        n = min(n, 4096)
+        first = rank * n
     scatter_diag = None
-    if args.origin == "root" and world > 1:
+    if args.origin == "root" and world > 1 and not args.dry_run:
         import shard
 
         # the batch originates on one GPU; each rank receives its
@@ -241,34 +406,53 @@ def main():
         dist.barrier()
         torch.cuda.synchronize(dev)
         ts = time.perf_counter()
-        local, ldescs, _ = shard.scatter_from_root(full, fdescs, coll_dev)
+        lbuf, ldescs, _ = shard.scatter_from_root(full, fdescs, coll_dev)
         torch.cuda.synchronize(dev)
         dist.barrier()
         t_sc = time.perf_counter() - ts
-        sent = torch.tensor([float(local.numel())], dtype=torch.float64, device=coll_dev)
+        sent = torch.tensor([float(lbuf.numel())], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(sent)
         scatter_diag = {"seconds": round(t_sc, 4), "bytes": int(sent[0]),
                         "GBps": round(float(sent[0]) / t_sc / 1e9, 2)}
-        b = workloads.Batch(args.workload, ldescs, int(local.numel()),
+        b = workloads.Batch(args.workload, ldescs, int(lbuf.numel()),
                             np.zeros(ldescs.size, np.uint8), 0,
                             int(np.maximum(ldescs["len"], 0).sum()))
-        base = torch.zeros((local.numel() + 15) // 16 * 16 + 16, dtype=torch.uint8, device=dev)
-        base[: local.numel()] = local.to(dev)
+        base = torch.zeros((lbuf.numel() + 15) // 16 * 16 + 16, dtype=torch.uint8, device=dev)
+        base[: lbuf.numel()] = lbuf.to(dev)
         descs = torch.from_numpy(ldescs.view(np.uint8).copy()).to(dev)
         out = torch.empty(max(b.n, 1), dtype=torch.int16, device=dev)
-        del full, local
+        del full, lbuf
     else:
         b = workloads.make(args.workload, n=n, first=first)
-        base, descs, out = workloads.to_device(b, dev)
-    stream = torch.cuda.current_stream(dev)
-    torch.cuda.synchronize(dev)
+        if args.dry_run:
+            base = descs = out = None
+        else:
+            base, descs, out = workloads.to_device(b, dev)
 
     # the batch's average packet length, as a caller that built it knows it
     len_hint = b.algo_bytes // max(1, b.n)
+    if args.dry_run:
+        stream = None
+        kernel = 0
 
-    def step():
-        lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(), stream.cuda_stream,
-                        kernel, args.unroll, args.waves_per_cu, len_hint)
+        def step():
+            pass
+
+        def sync():
+            pass
+    else:
+        import lvlip
+
+        stream = torch.cuda.current_stream(dev)
+        kernel = lvlip.KERNEL_NAMES[args.kernel]
+        torch.cuda.synchronize(dev)
+
+        def step():
+            lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(), stream.cuda_stream,
+                            kernel, args.unroll, args.waves_per_cu, len_hint)
+
+        def sync():
+            torch.cuda.synchronize(dev)
 
     # Bring the GPU to its sustained clocks before the W warm-up steps: from idle,
     # the first ~15 ms of launches run 5-25 % slow (scripts/warm_curve.py,
@@ -278,75 +462,101 @@ def main():
     # the GPUs do not idle between their settle and the timed region.
     if world > 1:
         dist.barrier()
-        torch.cuda.synchronize(dev)
+        sync()
     settle_n, ts = 0, time.perf_counter()
-    while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
+    while (time.perf_counter() - ts) * 1e3 < args.settle_ms and not args.dry_run:
         for _ in range(8):
             step()
         settle_n += 8
-        torch.cuda.synchronize(dev)
+        sync()
     settle_ms = (time.perf_counter() - ts) * 1e3
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
+    sync()
+    if not args.dry_run:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    e0.record(stream)
+    if not args.dry_run:
+        e0.record(stream)
     for _ in range(args.steps):
         step()
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
+    if not args.dry_run:
+        e1.record(stream)
+    sync()
     wall = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    kern_ms = e0.elapsed_time(e1) / args.steps  # events on the launch stream
+    kern_ms = e0.elapsed_time(e1) / args.steps if not args.dry_run else 0.0  # launch stream
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max, kern_ms_max = float(t[0]), float(t[1])
+    wall_max = float(t[0])
 
-    total_bytes = b.algo_bytes * world  # equal shards (uniform), near-equal for mixed
-    if world > 1 and (args.workload == "mixed" or args.workload in STRONG or args.origin == "root"):
-        tb = torch.tensor([float(b.algo_bytes)], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(tb)
-        total_bytes = float(tb[0])
-    value = total_bytes * args.steps / wall_max / 1e9
-    achieved = b.algo_bytes / (kern_ms / 1e3) / 1e9  # rank 0's kernel, algorithmic bytes
+    # every rank checks its whole timed batch (all N outputs) against the
+    # reference over the same bytes, copied back from HBM
+    cpus = host_cpus()
+    verify, first_chunk = None, None
+    if not args.no_verify and not args.dry_run:
+        thr = max(1, cpus["nproc"] // max(1, local_world))
+        verify, first_chunk = verify_timed_batch(
+            b, base, out, thr, keep_first=(rank == 0 and world == 1 and not args.no_cpu_baseline))
+        if not verify["ok"]:
+            log(f"bench.py rank {rank}: {verify['mismatches']} of {b.n} checksums differ from the reference")
+
+    # per-rank report: bytes, kernel time, verification
+    mine = {"bytes": b.algo_bytes, "descriptors": b.n, "kernel_ms": kern_ms,
+            "verified": None if verify is None else verify["ok"],
+            "mismatches": None if verify is None else verify["mismatches"]}
+    per_rank = [mine]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    total_bytes = sum(r["bytes"] for r in per_rank)
+    value = total_bytes * args.steps / wall_max / 1e9 if wall_max > 0 else 0.0
+    achieved = b.algo_bytes / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0  # rank 0's kernel
+    rank_ach = [r["bytes"] / (r["kernel_ms"] / 1e3) / 1e9 if r["kernel_ms"] > 0 else 0.0 for r in per_rank]
+    for r, info, a in zip(per_rank, ranks, rank_ach):
+        info.update({"kernel_ms": round(r["kernel_ms"], 5), "kernel_GBps": round(a, 2),
+                     "descriptors": r["descriptors"], "verified": r["verified"]})
+    verified = None
+    if all(r["verified"] is not None for r in per_rank):
+        verified = all(r["verified"] for r in per_rank)
+
     kernel_label = f"{args.kernel}-u{args.unroll}-w{args.waves_per_cu}"
-    # AUTO's choice (dispatch_one in csum_kernels.hip): the interleaved stream
-    # from 896 B, lane groups up to 32 B, the flat sweep between
     chosen = args.kernel
-    if kernel == lvlip.KERNEL_AUTO:
-        chosen = "window" if len_hint >= 896 else ("lane" if 0 < len_hint <= 32 else "flat")
+    if not args.dry_run and kernel == 0:
+        chosen = lvlip.auto_kernel_name(len_hint, b.n)
 
     diag = {"settle": {"launches": settle_n, "ms": round(settle_ms, 1)}}
+    if verify is not None:
+        diag["verify"] = verify
     if scatter_diag is not None:
         diag["scatter"] = scatter_diag
-    if rank == 0 and args.sweep:
-        diag["sweep"] = sweep(lvlip, torch, base, descs, out, b, stream)
-    if rank == 0 and base.numel() < (1 << 34):
-        diag["read_probe_GBps"] = read_probe(lvlip, torch, base, stream)
-    if rank == 0 and args.frames:
-        diag["frames_dev"] = frames_dev(lvlip, torch, dev)
-    if rank == 0 and args.e2e:
-        diag["e2e_host_GBps"] = e2e(lvlip, b, base)
-        diag["latency_us"] = latency(lvlip, torch, dev)
+    if rank == 0 and not args.dry_run:
+        if args.sweep:
+            diag["sweep"] = sweep(lvlip, torch, base, descs, out, b, stream)
+        if base.numel() < (1 << 34):
+            diag["read_probe_GBps"] = read_probe(lvlip, torch, base, stream)
+        if args.frames:
+            diag["frames_dev"] = frames_dev(lvlip, torch, dev)
+        if args.e2e:
+            diag["e2e_host_GBps"] = e2e(lvlip, b, base)
+            diag["latency_us"] = latency(lvlip, torch, dev)
 
-    cpu, verified = None, None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, verified = cpu_baseline(b, threads=min(16, os.cpu_count() or 1), kernel=kernel,
-                                     unroll=args.unroll, wpc=args.waves_per_cu, dev=dev,
-                                     len_hint=len_hint)
+    cpu = None
+    if rank == 0 and world == 1 and first_chunk is not None:
+        cpu = cpu_baseline(b, first_chunk, cpus)
 
     if rank == 0:
         rec = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+            "metric": METRIC, "value": None if args.dry_run else round(value, 2), "unit": "GB/s",
+            "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(wall_max * 1e3 / args.steps, 4),
+            "ms_per_step": None if args.dry_run else round(wall_max * 1e3 / args.steps, 4),
             "higher_is_better": True, "scaling": "strong" if args.workload in STRONG else "weak",
             "vs_baseline": None, "dtype": "u16",
             "data": "synthetic (splitmix64 seed 0x1E7E1C5, 1% all-0x00 + 1% all-0xff packets), "
@@ -357,17 +567,27 @@ def main():
                        "len_hint": len_hint, "parallelism": f"shard{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "frac_aggregate": round(value / (world * HBM_PEAK_GBPS), 4),
+                         "frac_min_rank": round(min(rank_ach) / HBM_PEAK_GBPS, 4),
                          "traffic": traffic_from_profiles(args.workload, kernel_label,
                                                           KERNEL_FN.get(chosen, "")),
                          "kernel_ms": round(kern_ms, 5),
                          "algo_bytes_per_launch": b.algo_bytes},
             "cpu_baseline": cpu,
             "verified_bit_exact": verified,
+            "dist": {"world_size": dist.get_world_size() if world > 1 else 1,
+                     "backend": backend if world > 1 else None, "launcher": launcher,
+                     "shared_devices": len({(r["host"], r.get("pci")) for r in ranks}) < world,
+                     "ranks": ranks},
             "diag": diag,
         }
+        if args.dry_run:
+            rec["dry_run"] = True
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if verified is False:
+        raise SystemExit("bench.py: the timed batch's checksums differ from the reference")
 
 
 def timed(torch, fn, stream, reps=20, warm=3):
@@ -431,28 +651,15 @@ def frames_dev(lvlip, torch, dev):
     res = {}
     for name, fn, nbytes in (
             ("tx_fill", lambda: lvlip.tx_checksum_dev(base, fdt, stream=stream), 20 * n + l4_bytes),
-            # A/B: the same with plain (temporal) field stores
-            ("tx_fill_plain", lambda: lvlip.tx_checksum_dev(base, fdt, stream=stream), 20 * n + l4_bytes),
+            # A/B (liblvlip_lab.so): the same with plain (temporal) field stores
+            ("tx_fill_plain", lambda: lvlip.frames_variant_dev(0, 1, base, fdt, stream=stream),
+             20 * n + l4_bytes),
             ("rx_header", lambda: lvlip.rx_verify_dev(base, fdt, 0, stream=stream), 20 * n),
-            # the header call's A/B kernel (k_flat2 with a frame source)
-            ("rx_header_flat", lambda: lvlip.rx_verify_dev(base, fdt, 0, stream=stream), 20 * n),
+            # A/B: the header call on k_flat2 with a frame source
+            ("rx_header_flat", lambda: lvlip.frames_variant_dev(1, 0, base, fdt, stream=stream), 20 * n),
             ("rx_header_l4", lambda: lvlip.rx_verify_dev(base, fdt, lvlip.RX_VERIFY_L4, stream=stream),
              20 * n + l4_bytes)):
-        # the A/B kernels are selected by knobs the library reads per call;
-        # the caller's own settings come back afterwards
-        knob = {"rx_header_flat": ("LVLIP_FRAMES_RX_HDR", "flat"),
-                "tx_fill_plain": ("LVLIP_FRAMES_TX_STORE", "plain")}.get(name)
-        saved = os.environ.get(knob[0]) if knob else None
-        if knob:
-            os.environ[knob[0]] = knob[1]
-        try:
-            ms = timed(torch, fn, stream, reps=10)
-        finally:
-            if knob:
-                if saved is None:
-                    os.environ.pop(knob[0], None)
-                else:
-                    os.environ[knob[0]] = saved
+        ms = timed(torch, fn, stream, reps=10)
         res[name] = {"ms": round(ms, 4), "Mframes_per_s": round(n / ms / 1e3, 1),
                      "GBps": round(nbytes / ms / 1e6, 1)}
     v = lvlip.rx_verify_dev(base, fdt, 0, stream=stream)

@@ -121,43 +121,31 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
 
 /* Kernel selection for lvlip_csum_batch_dev_ex.  AUTO picks by len_hint:
  * >= 896 B -> WINDOW (shape by the hint); 1-32 B -> LANE; otherwise or
- * unknown -> FLAT (measured: DESIGN.md §4-5). */
+ * unknown -> FLAT (measured: DESIGN.md §4-5).  lvlip_auto_kernel() tells
+ * which kernel and shape AUTO runs.  Ids 1, 2, 4, 5, 6, 7 and 9 are the A/B
+ * variants measured against these (liblvlip_lab.so, not this library): here
+ * they return LVLIP_EINVAL. */
 #define LVLIP_KERNEL_AUTO        0  /* the default                                 */
-#define LVLIP_KERNEL_WAVE        1  /* one wavefront per packet, persistent stream,
-                                       contiguous ranges per wave (A/B)        */
-#define LVLIP_KERNEL_WAVE_LDS    2  /* one wave per packet, LDS-DMA staging (A/B)  */
 #define LVLIP_KERNEL_FLAT        3  /* chunk-balanced tile sweep (ragged batches)  */
-#define LVLIP_KERNEL_WAVE_SIMPLE 4  /* one wave per packet, one launch wave each   */
-#define LVLIP_KERNEL_WAVE_STATIC 6  /* retired round-1 A/B id: runs WAVE         */
-#define LVLIP_KERNEL_WAVE_DYN    7  /* retired round-1 A/B id (dynamic tail,
-                                       DESIGN.md §8): runs WAVE                */
-#define LVLIP_KERNEL_WINDOW      8  /* WAVE with packets dealt in small groups
-                                       round robin over the grid (one narrow
-                                       window of the batch in flight)          */
-#define LVLIP_KERNEL_WFLAT       9  /* FLAT's chunk sweep, one wave per tile of
-                                       descriptors, tiles dealt round robin    */
+#define LVLIP_KERNEL_WINDOW      8  /* one wavefront per packet, persistent, packets
+                                       dealt in small groups round robin over the
+                                       grid (one narrow window of the batch in
+                                       flight)                                 */
 #define LVLIP_KERNEL_LANE       10  /* a few lanes per packet, chunks summed in
                                        registers (batches of small packets)   */
 
 typedef struct lvlip_launch_cfg {
     int32_t  kernel;        /* LVLIP_KERNEL_*                               */
-    int32_t  unroll;        /* 16-B loads in flight per lane (0 = default);
-                               WAVE, WINDOW: 2-KiB pieces in flight per
-                               wave; WINDOW: | packets per group << 8
+    int32_t  unroll;        /* 0 = default.  WINDOW: 2-KiB pieces in flight
+                               per wave (2, 3, 4) | packets per group << 8
                                (1, 2, 3, 4 or 8; 0 = by len_hint);
-                               WFLAT: 64-chunk loads per round | descriptors
-                               per tile << 8 (16, 32 or 64; 0 = 32);
-                               FLAT: 64-chunk loads per round | group order
-                               << 8 (1 interleaved, 2 quarters, 3 blocks;
-                               0 = LVLIP_FLAT_GROUPS, else quarters) | 1 << 10
-                               for tiles of 512 descriptors (A/B; U 4 or 8,
-                               quarters or blocks);
+                               FLAT: 64-chunk loads per round (2, 4, 8);
                                LANE: packets per lane group | 16-B chunks
                                per lane << 8 | lanes per packet << 16 (1, 2,
-                               4, 8); longer packets go to a whole-wave
-                               loop (0 = 4 | 2 << 8 | 2 << 16)              */
-    int32_t  waves_per_cu;  /* WAVE: resident waves per CU (0 = 8); others:
-                               grid cap (0 = one wave per packet)           */
+                               4, 8) | unconditional loads << 24; longer
+                               packets go to a whole-wave loop (0 = 4 | 2 << 8
+                               | 2 << 16)                                   */
+    int32_t  waves_per_cu;  /* WINDOW: resident waves per CU (0 = 8)        */
     int32_t  len_hint;      /* average packet length in bytes if the caller
                                knows it (AUTO uses it), 0 = unknown         */
 } lvlip_launch_cfg;
@@ -165,6 +153,12 @@ typedef struct lvlip_launch_cfg {
 int lvlip_csum_batch_dev_ex(const void *base, const lvlip_csum_desc *descs,
                             uint32_t n, uint16_t *out, void *stream,
                             const lvlip_launch_cfg *cfg);
+
+/* The kernel and launch shape LVLIP_KERNEL_AUTO runs for n descriptors of
+ * average length len_hint on the current HIP device: returns the kernel id
+ * and, when resolved != NULL, fills it with that id, its unroll and
+ * waves_per_cu words and len_hint. */
+int lvlip_auto_kernel(int32_t len_hint, uint32_t n, lvlip_launch_cfg *resolved);
 
 /* ======================================================================= */
 /* Group 3: host-resident batches (per-thread context)                      */
@@ -231,6 +225,10 @@ int lvlip_abi_version(void);
 int lvlip_device_count(void);
 /* Last HIP error string recorded by this library in the calling thread. */
 const char *lvlip_last_hip_error(void);
+/* Hash of the sources this library was built from (the files listed in
+ * level-ip_amd/BUILD_SOURCES, SHA-256, first 16 hex digits): the tests and
+ * the bench refuse a library whose hash differs from the tree's. */
+const char *lvlip_build_id(void);
 
 #pragma GCC visibility pop
 #ifdef __cplusplus

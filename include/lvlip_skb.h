@@ -115,7 +115,33 @@ uint32_t lvlip_icmp_echo_reply_csum(uint16_t req_csum);
  * request. */
 uint32_t lvlip_icmp_echo_reply_fill(lvlip_frame *frames, uint32_t n);
 
-/* ---- f1/f2 on device-resident frames ------------------------------------ */
+/* ---- f1/f2 over level-ip's own skb queues -------------------------------- */
+
+/* The same calls over an sk_buff_head (include/skbuff.h:25-29) as level-ip
+ * fills it, walked in list order through the intrusive list_head at the start
+ * of every sk_buff (include/list.h; LP64 offsets of include/skbuff.h:9-23:
+ * len 40, end 56, head 64, data 72).  The queue is only read.
+ *
+ * RX: skbs as netdev_rx_loop allocates and fills them (src/netdev.c:86-101,
+ * alloc_skb src/skbuff.c:5-20): the frame is skb->data .. skb->end (tun_read
+ * writes it at skb->data; the rest of the BUFLEN buffer is zero).  verdict[k]
+ * is the k-th skb's; cap is verdict's capacity.  Returns the number of skbs,
+ * LVLIP_ERANGE if more than cap, or LVLIP_E*. */
+struct sk_buff_head;
+int lvlip_rx_verify_skb_list(lvlip_csum_ctx *ctx, struct sk_buff_head *q, uint32_t flags,
+                             uint8_t *verdict, uint32_t cap);
+
+/* TX: skbs as ip_output leaves them before dst_neigh_output
+ * (src/ip_output.c:14-56): skb->data at the IPv4 header, skb->len covering it
+ * and the TCP/ICMP segment, the Ethernet header's 14 bytes reserved in front
+ * (the frame is skb->data - 14 .. skb->data + skb->len).  Fills the TCP/ICMP
+ * and IPv4 checksums as lvlip_tx_checksum, i.e. what tcp_transmit_skb
+ * (src/tcp_output.c:126), icmpv4_reply (src/icmpv4.c:47) and ip_send_check
+ * (src/ip_output.c:53) would have stored.  Returns the number of skbs or
+ * LVLIP_E* (skbs untouched on error). */
+int lvlip_tx_checksum_skb_list(lvlip_csum_ctx *ctx, struct sk_buff_head *q);
+
+/* ---- f1/f2/f4 on device-resident frames ---------------------------------- */
 
 /* Frames already in HBM (a receive ring filled by a GPU-direct NIC, or frames
  * built on the GPU): one frame = `len` bytes at base + offset, Ethernet header
@@ -141,6 +167,17 @@ int lvlip_rx_verify_dev(const void *base, const lvlip_frame_desc *frames, uint32
  * filled); status may be NULL. */
 int lvlip_tx_checksum_dev(void *base, const lvlip_frame_desc *frames, uint32_t n,
                           uint8_t *status, void *workspace, void *stream);
+
+/* f4 on frames in HBM: lvlip_icmp_echo_reply_fill in one launch, one lane per
+ * frame.  Every frame that is an IPv4 ICMP echo request (type 8, code 0, the
+ * message inside the frame) whose ICMP checksum verified becomes the reply's
+ * ICMP part: type 0 and the RFC 1624 checksum field, bit-identical to
+ * icmpv4_reply's full recomputation (src/icmpv4.c:44-47); in the one
+ * undecidable case (LVLIP_CSUM_RECOMPUTE) the lane sums the message itself.
+ * status[i] (may be NULL): 1 updated from the field, 2 recomputed, 0 not an
+ * echo request (frame untouched).  Nothing else of the message is read. */
+int lvlip_icmp_echo_reply_dev(void *base, const lvlip_frame_desc *frames, uint32_t n,
+                              uint8_t *status, void *stream);
 
 /* RFC 1071 pseudo-header seed with the carries folded back (for RX verify of
  * checksums produced by RFC-correct peers). */

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <condition_variable>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -28,7 +29,11 @@ class GatherPool {
         cv_job_.notify_all();
         for (auto& t : th_) t.join();
     }
-    // fn(0 .. parts-1), part 0 on the calling thread; returns when all are done
+    // fn(0 .. parts-1), part 0 on the calling thread; returns when all are done.
+    // Workers that cannot be started (std::thread throws std::system_error
+    // under a thread limit) are not an error: their parts run on the calling
+    // thread after part 0, so the call still completes (never std::terminate
+    // through the C ABI).
     void run(int parts, const std::function<void(int)>& fn) {
         if (parts <= 1) {
             fn(0);
@@ -39,17 +44,23 @@ class GatherPool {
             // thread is gen_'s only writer, so it may read it unlocked)
             const int id = (int)th_.size() + 1;
             const uint64_t g0 = gen_;
-            th_.emplace_back([this, id, g0] { worker(id, g0); });
+            try {
+                th_.emplace_back([this, id, g0] { worker(id, g0); });
+            } catch (const std::exception&) {
+                break;
+            }
         }
+        const int w = (int)th_.size() < parts - 1 ? (int)th_.size() : parts - 1;  // parts 1..w
         {
             std::lock_guard<std::mutex> g(m_);
             job_ = &fn;
-            parts_ = parts;
-            pending_ = parts - 1;
+            parts_ = w + 1;
+            pending_ = w;
             ++gen_;
         }
         cv_job_.notify_all();
         fn(0);
+        for (int p = w + 1; p < parts; ++p) fn(p);
         std::unique_lock<std::mutex> g(m_);
         cv_done_.wait(g, [this] { return pending_ == 0; });
         job_ = nullptr;

@@ -1,0 +1,808 @@
+// lab_kernels.hip — the A/B kernels of DESIGN.md §4, §8, §9 (liblvlip_lab.so,
+// diagnostics; the product library does not contain them).
+//
+//   k_stream       the ring of k_window with contiguous per-wave ranges
+//                  (LVLIP_KERNEL_WAVE = 1), in five load policies
+//   k_wave_simple  one wave per packet, one launch wave each (4)
+//   k_wave_lds     the same with LDS-DMA staging (2)
+//   k_flat         the first flat kernel: binary search, ds_bpermute
+//                  segmented scan (5)
+//   k_wflat        k_flat2's sweep one wave per tile, tiles dealt round robin (9)
+//   k_flat2        its other shapes (3): group orders, tiles of 512, temporal
+//                  loads, U 6 / 12, an LDS pad; and the frame calls' variants
+//                  (8 loads per round, block order, plain field stores, the
+//                  flat sweep for the header-only RX call)
+//
+// Entry points (C ABI, used by bench.py --sweep and scripts/ through
+// lvlip.py): lvlip_lab_batch_dev_ex takes the kernel ids above with
+// lvlip_launch_cfg's encodings; lvlip_lab_frames_dev the frame-call variants.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "csum_dev.h"
+
+namespace lvlip {
+
+template <int U>
+__global__ __launch_bounds__(256) void k_wave_simple(const uint8_t* __restrict__ base,
+                                              const lvlip_csum_desc* __restrict__ descs,
+                                              uint32_t n, uint16_t* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint64_t stride = (uint64_t)gridDim.x * wpb;
+    // 64-bit cursor: with n near LVLIP_MAX_BATCH a u32 p + stride would wrap
+    for (uint64_t p = uniform(blockIdx.x * wpb + (threadIdx.x >> 6)); p < n; p += stride) {
+        const lvlip_csum_desc d = descs[p];
+        uint32_t w = 0;
+        if (d.len > 0) {
+            const uint64_t a0 = d.offset & ~15ull;
+            const int lo = (int)(d.offset & 15ull);
+            const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
+            const uint32_t nch = (uint32_t)((span + 15u) >> 4);
+            const uint32_t last_valid = (uint32_t)(span - 16ull * (nch - 1u));  // 1..16
+            const uint4* src = reinterpret_cast<const uint4*>(base + a0);
+            w = (d.offset & 1ull) ? wave_packet_sum<U, true>(src, nch, lo, last_valid, lane)
+                                  : wave_packet_sum<U, false>(src, nch, lo, last_valid, lane);
+        }
+        w = wave_sum(w);
+        if (lane == 0) out[p] = finish(d.start_sum, w);
+    }
+}
+
+// POL: the data loads' cache policy (A/B, LVLIP_LOAD_POLICY)
+template <int R, int POL = 0>
+__global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ base,
+                                                const lvlip_csum_desc* __restrict__ descs,
+                                                uint32_t n, uint16_t* __restrict__ out) {
+    __shared__ uint4 s_win[SW_WAVES][2][64];
+    ring_sweep<R, 0, POL>(base, descs, n, out, s_win[uniform(threadIdx.x >> 6)]);
+}
+
+// ------------------------------------------------- k_wave_lds (LDS-DMA path) --
+
+template <int U, bool ODD>
+__device__ __forceinline__ uint32_t wave_packet_sum_lds(const uint8_t* __restrict__ src,
+                                                        uint32_t nch, int lo,
+                                                        uint32_t last_valid, uint32_t lane,
+                                                        uint4* slab /* U*64 chunks */) {
+    uint32_t acc = 0;
+    for (uint32_t c0 = 0; c0 < nch; c0 += 64u * U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * 64u + lane;
+            // LDS destination is wave-uniform base + lane*16; the global source is
+            // per lane.  Lanes past the packet re-read its first chunk (harmless,
+            // in range) and are zeroed below.
+            const uint8_t* g = src + 16ull * (c < nch ? c : 0u);
+            __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)(slab + u * 64), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * 64u + lane;
+            uint4 v = slab[u * 64 + lane];
+            if (c >= nch) v = make_uint4(0u, 0u, 0u, 0u);
+            if (c == 0u || c == nch - 1u) {
+                const int b0 = (c == 0u) ? lo : 0;
+                const int b1 = (c == nch - 1u) ? (int)last_valid : 16;
+                v = mask_chunk(v, b0, b1);
+            }
+            acc += chunk_words<ODD>(v);
+        }
+        // WAR: every lane's ds_read of this round must land before the next
+        // round's DMA overwrites the slab.
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return acc;
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_wave_lds(const uint8_t* __restrict__ base,
+                                                  const lvlip_csum_desc* __restrict__ descs,
+                                                  uint32_t n, uint16_t* __restrict__ out) {
+    __shared__ uint4 slabs[4 * U * 64];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = uniform(threadIdx.x >> 6);
+    uint4* slab = slabs + wid * (U * 64);
+    const uint64_t stride = (uint64_t)gridDim.x * 4u;
+    for (uint64_t p = uniform(blockIdx.x * 4u + wid); p < n; p += stride) {
+        const lvlip_csum_desc d = descs[p];
+        uint32_t w = 0;
+        if (d.len > 0) {
+            const uint64_t a0 = d.offset & ~15ull;
+            const int lo = (int)(d.offset & 15ull);
+            const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
+            const uint32_t nch = (uint32_t)((span + 15u) >> 4);
+            const uint32_t last_valid = (uint32_t)(span - 16ull * (nch - 1u));
+            w = (d.offset & 1ull)
+                    ? wave_packet_sum_lds<U, true>(base + a0, nch, lo, last_valid, lane, slab)
+                    : wave_packet_sum_lds<U, false>(base + a0, nch, lo, last_valid, lane, slab);
+        }
+        w = wave_sum(w);
+        if (lane == 0) out[p] = finish(d.start_sum, w);
+    }
+}
+
+// ------------------------------------------------------ k_flat (ragged path) --
+
+constexpr int FLAT_T = 256;                 // threads = descriptors per tile
+constexpr uint32_t FLAT_MAX_CHUNKS = 1u << 16;  // bigger packets: whole-wave path
+
+template <bool ODD>
+__device__ __forceinline__ uint32_t words_of(uint4 v) { return chunk_words<ODD>(v); }
+
+__global__ __launch_bounds__(FLAT_T) void k_flat(const uint8_t* __restrict__ base,
+                                                 const lvlip_csum_desc* __restrict__ descs,
+                                                 uint32_t n, uint16_t* __restrict__ out) {
+    __shared__ uint32_t s_cstart[FLAT_T + 1];  // chunk prefix (exclusive), [T] = total
+    __shared__ uint64_t s_a0[FLAT_T];          // 16-B aligned start offset
+    __shared__ uint32_t s_meta[FLAT_T];        // lo | last_valid<<4 | odd<<9 | big<<10
+    __shared__ uint32_t s_acc[FLAT_T];
+    __shared__ uint32_t s_wsum[FLAT_T / 64];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wid = tid >> 6;
+    const uint32_t tile0 = blockIdx.x * (uint32_t)FLAT_T;
+    const uint32_t i_me = tile0 + tid;
+
+    // 1. descriptor metadata + chunk counts
+    uint32_t nch = 0, meta = 0;
+    uint64_t a0 = 0;
+    uint32_t start_sum = 0;
+    bool big = false;
+    if (i_me < n) {
+        const lvlip_csum_desc d = descs[i_me];
+        start_sum = d.start_sum;
+        if (d.len > 0) {
+            a0 = d.offset & ~15ull;
+            const uint32_t lo = (uint32_t)(d.offset & 15ull);
+            const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
+            const uint64_t nch64 = (span + 15u) >> 4;
+            const uint32_t last_valid = (uint32_t)(span - 16ull * (nch64 - 1u));
+            big = nch64 > FLAT_MAX_CHUNKS;
+            nch = big ? 0u : (uint32_t)nch64;
+            meta = lo | (last_valid << 4) | ((uint32_t)(d.offset & 1ull) << 9) |
+                   ((uint32_t)big << 10);
+        }
+    }
+    s_a0[tid] = a0;
+    s_meta[tid] = meta;
+    s_acc[tid] = 0;
+
+    // 2. exclusive prefix sum of nch over the tile (wave scan + wave totals)
+    uint32_t incl = nch;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl += t;
+    }
+    if (lane == 63) s_wsum[wid] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t k = 0; k < wid; ++k) wbase += s_wsum[k];
+    s_cstart[tid] = wbase + incl - nch;
+    if (tid == FLAT_T - 1) s_cstart[FLAT_T] = wbase + incl;
+    __syncthreads();
+
+    // 3. sweep the tile's chunks: lane j takes chunk j (coalesced across packets)
+    const uint32_t total = s_cstart[FLAT_T];
+    for (uint32_t j0 = wid * 64u; j0 < total; j0 += FLAT_T) {
+        const uint32_t j = j0 + lane;
+        uint32_t i = FLAT_T;  // sentinel for lanes past the end
+        uint32_t val = 0;
+        if (j < total) {
+            // largest i with cstart[i] <= j (skips empty descriptors)
+            i = 0;
+#pragma unroll
+            for (uint32_t step = FLAT_T / 2; step > 0; step >>= 1)
+                if (s_cstart[i + step] <= j) i += step;
+            const uint32_t k = j - s_cstart[i];
+            const uint32_t m = s_meta[i];
+            const uint32_t ni = s_cstart[i + 1] - s_cstart[i];
+            uint4 v = *reinterpret_cast<const uint4*>(base + s_a0[i] + 16ull * k);
+            if (k == 0u || k == ni - 1u) {
+                const int b0 = (k == 0u) ? (int)(m & 15u) : 0;
+                const int b1 = (k == ni - 1u) ? (int)((m >> 4) & 31u) : 16;
+                v = mask_chunk(v, b0, b1);
+            }
+            val = (m & (1u << 9)) ? chunk_words<true>(v) : chunk_words<false>(v);
+        }
+        // segmented reduction keyed by i (non-decreasing across lanes)
+        const uint32_t i_first = __shfl(i, 0, 64);
+        const uint32_t i_last = __shfl(i, 63, 64);
+        if (i_first == i_last) {
+            val = wave_sum(val);
+            if (lane == 0 && i_first < (uint32_t)FLAT_T) atomicAdd(&s_acc[i_first], val);
+        } else {
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t v2 = __shfl_up(val, off, 64);
+                const uint32_t i2 = __shfl_up(i, off, 64);
+                if (lane >= (uint32_t)off && i2 == i) val += v2;
+            }
+            const uint32_t i_next = __shfl_down(i, 1, 64);
+            const bool tail = (lane == 63u) || (i_next != i);
+            if (tail && i < (uint32_t)FLAT_T) atomicAdd(&s_acc[i], val);
+        }
+    }
+
+    // 4. packets too big for the tile sweep: one wave each
+    __syncthreads();
+    for (uint32_t q = 0; q < (uint32_t)FLAT_T; ++q) {
+        if (!(s_meta[q] & (1u << 10))) continue;  // uniform: LDS broadcast
+        if ((q & 3u) != wid) continue;
+        const uint32_t m = s_meta[q];
+        const lvlip_csum_desc d = descs[tile0 + q];
+        const uint64_t span = (uint64_t)(m & 15u) + (uint64_t)(uint32_t)d.len;
+        const uint32_t nchq = (uint32_t)((span + 15u) >> 4);
+        const uint4* src = reinterpret_cast<const uint4*>(base + s_a0[q]);
+        uint32_t w = (m & (1u << 9))
+                         ? wave_packet_sum<2, true>(src, nchq, (int)(m & 15u), (m >> 4) & 31u, lane)
+                         : wave_packet_sum<2, false>(src, nchq, (int)(m & 15u), (m >> 4) & 31u, lane);
+        w = wave_sum(w);
+        if (lane == 0) s_acc[q] = w;
+    }
+    __syncthreads();
+
+    // 5. fold and store (coalesced 2-B stores)
+    if (i_me < n) out[i_me] = finish(start_sum, s_acc[tid]);
+}
+
+// ------------------------------------------- k_wflat (ragged, window deal) --
+//
+// k_flat2's chunk sweep, one wave per tile of D descriptors, with the tiles
+// dealt round robin over the grid as k_window deals its packet groups: wave
+// rank r (XCD-major) sweeps tiles r, r + nw, r + 2 nw, ...  A k_flat2 workgroup
+// owns 256 descriptors (~100 KB of a mixed batch) and its four waves sweep
+// contiguous quarters of them, so the waves in flight read ~8 000 streams over
+// ~200 MB; here the waves in flight read one window of nw x D descriptors
+// (~13-25 MB of a mixed batch) that slides through the batch.  The read probes
+// on the mixed buffer measure that order 4.7 % faster (scripts/lab_window.py,
+// DESIGN.md §4).
+//
+// Per tile, all in one wave (no workgroup barrier):
+//   1. lane i < D reads descriptor i; chunk counts, an exclusive wave scan of
+//      them (the tile's virtual chunk space), a rank among the non-empty small
+//      descriptors (mbcnt of a ballot), records by rank and a head bitmap per
+//      64-chunk load in the wave's LDS;
+//   2. the sweep: U loads of 64 chunks per round, every lane's packet found as
+//      in k_flat2 (heads before the load + mbcnt), bytes outside the packet
+//      masked in the lane (its first and last chunk), odd-address packets
+//      byte-swapped, and segment sums by the inclusive-scan trick into the
+//      descriptor's LDS accumulator;
+//   3. descriptors longer than WCAP chunks: one wave-per-packet loop each;
+//   4. fold, ~, one store of the tile's D results.
+constexpr uint32_t WCAP = 128;  // chunks of the largest swept descriptor (2 KiB)
+
+template <int D>
+struct WflatLds {
+    uint4 rec[SW_WAVES][D];                 // by rank: {a0 lo, a0 hi, cstart, meta}
+    uint2 msk[SW_WAVES][D * WCAP / 64];     // head bitmap per 64-chunk load
+    uint32_t acc[SW_WAVES][D];              // by descriptor
+    uint4 edge[SW_WAVES][2 * D];            // by descriptor: raw first / last chunk
+};
+
+// Orders this wave's LDS traffic across lanes (a lane reading what another
+// lane wrote): LDS ops of one wave execute in order, so the compiler only has
+// to be kept from moving them, and the counter drained.  No vmcnt: global
+// loads in flight stay in flight.
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int U, int D>
+__global__ __launch_bounds__(256) void k_wflat(const uint8_t* __restrict__ base,
+                                               const lvlip_csum_desc* __restrict__ descs,
+                                               uint32_t n, uint16_t* __restrict__ out) {
+    static_assert(D >= 1 && D <= 64, "one descriptor per lane");
+    __shared__ WflatLds<D> L;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = uniform(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * SW_WAVES;
+    const uint64_t rank =
+        (gridDim.x & 7u) == 0u
+            ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * SW_WAVES + wid
+            : (uint64_t)blockIdx.x * SW_WAVES + wid;
+    const uint64_t ntiles = ((uint64_t)n + D - 1) / D;
+    uint4* s_rec = L.rec[wid];
+    uint2* s_msk = L.msk[wid];
+    uint32_t* s_acc = L.acc[wid];
+    uint4* s_edge = L.edge[wid];
+
+    // descriptors of the wave's next tile, one 16-B load per lane issued a tile
+    // ahead (lanes past the batch re-read its last descriptor)
+    // Issued from asm, so hipcc's wait-count pass does not see it in flight and
+    // drain it before the sweep's first loads; the sweep's own waits retire it
+    // (vector memory ops retire in issue order), and the loop head waits for it
+    // explicitly, which costs nothing after a tile that had a sweep round.
+    auto fetch = [&](uint64_t t, u32x4& d) {
+        uint64_t i = t * D + (lane < (uint32_t)D ? lane : 0u);
+        i = i < n ? i : n - 1u;
+        const lvlip_csum_desc* g = descs + i;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(g) : "memory");
+    };
+    u32x4 dnext;
+    fetch(rank < ntiles ? rank : 0u, dnext);
+    // the previous tile's results, stored once the next prefetch is retired
+    uint64_t i_prev = 0;
+    bool st_prev = false;
+    uint16_t res_prev = 0;
+    for (uint64_t t = rank; t < ntiles; t += nw) {
+        const uint64_t i = t * D + lane;
+        const bool mine = lane < (uint32_t)D && i < n;
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(dnext) : : "memory");
+        const u32x4 dv = dnext;  // {offset lo, offset hi, len, start_sum}
+        // the previous tile's store and the next tile's prefetch go out behind
+        // this tile's first sweep loads, so they share their round trip (the
+        // store's data register is reused soon after, and the wait hipcc puts
+        // before that reuse drains everything in flight)
+        bool side_done = false;
+        auto side = [&]() {
+            if (st_prev) out[i_prev] = res_prev;
+            st_prev = false;
+            if (t + nw < ntiles) fetch(t + nw, dnext);
+            side_done = true;
+        };
+        // ---- 1. descriptors -> chunk space, records, head bitmap
+        uint32_t start_sum = 0, nch = 0, meta = 0;
+        uint64_t a0 = 0;
+        bool big = false;
+        if (mine) {
+            lvlip_csum_desc d;
+            d.offset = ((uint64_t)dv.y << 32) | dv.x;
+            d.len = (int32_t)dv.z;
+            d.start_sum = dv.w;
+            start_sum = d.start_sum;
+            if (d.len > 0) {
+                const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
+                a0 = abs & ~15ull;
+                const uint32_t lo = (uint32_t)(abs & 15ull);
+                const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
+                const uint64_t c64 = (span + 15u) >> 4;
+                const uint32_t lastv = (uint32_t)(span - 16ull * (c64 - 1u));  // 1..16
+                big = c64 > WCAP;
+                nch = big ? 0u : (uint32_t)c64;
+                // edge flags: the sweep stashes the first (bit 24) and last (bit
+                // 25) chunk in LDS when they hold bytes outside the descriptor,
+                // and step 4 subtracts those bytes (as k_flat2)
+                const bool ef = !big && (lo != 0u || (c64 == 1u && lastv != 16u));
+                const bool el = !big && c64 > 1u && lastv != 16u;
+                // meta: nch (8 bits) | lo << 8 | lastv << 12 | odd << 17 | lane << 18 | ef, el
+                meta = nch | (lo << 8) | (lastv << 12) | ((uint32_t)(abs & 1ull) << 17) | (lane << 18) |
+                       ((uint32_t)ef << 24) | ((uint32_t)el << 25);
+            }
+        }
+        const uint32_t incl = wave_incl_scan(nch);
+        const uint32_t C = uniform((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
+        const uint32_t cstart = incl - nch;
+        const uint64_t nz = __builtin_amdgcn_ballot_w64(nch != 0u);
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
+        const uint32_t nloads = (C + 63u) >> 6;
+        for (uint32_t q = lane; q < nloads; q += 64u) s_msk[q] = make_uint2(0u, 0u);
+        if (lane < (uint32_t)D) s_acc[lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (nch) {
+            s_rec[r] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), cstart, meta);
+            const uint32_t q = cstart >> 6, b = cstart & 63u;
+            if (b < 32u) atomicOr(&s_msk[q].x, 1u << b);
+            else atomicOr(&s_msk[q].y, 1u << (b - 32u));
+        }
+        lds_sync();
+
+        // ---- 2. sweep the tile's chunk space, U loads of 64 chunks per round
+        uint32_t heads = 0;  // heads in the loads before this round
+        for (uint32_t u0 = 0; u0 < nloads; u0 += U) {
+            uint32_t hb[U], hlo[U], hhi[U];
+            bool gv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                gv[u] = u0 + u < nloads;
+                const uint2 m = s_msk[gv[u] ? u0 + u : nloads - 1u];
+                hlo[u] = uniform(m.x);
+                hhi[u] = uniform(m.y);
+                hb[u] = heads;
+                heads += gv[u] ? (uint32_t)__popcll(((uint64_t)hhi[u] << 32) | hlo[u]) : 0u;
+            }
+            uint4 x[U], rec[U];
+            uint32_t kk[U];
+            bool vl[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = (u0 + u) * 64u + lane;
+                vl[u] = gv[u] && c < C;
+                const uint64_t H = ((uint64_t)hhi[u] << 32) | hlo[u];
+                const uint64_t Hs = H >> 1;
+                const uint32_t cnt = __builtin_amdgcn_mbcnt_hi((uint32_t)(Hs >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)Hs, 0u));
+                // a valid chunk's packet: heads at or below it - 1 (chunk 0 is a
+                // head); lanes past the chunk space read record 0's first chunk,
+                // a valid address, and are zeroed
+                const uint32_t rk = hb[u] + (uint32_t)(H & 1ull) + cnt - 1u;
+                rec[u] = s_rec[vl[u] ? rk : 0u];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = (u0 + u) * 64u + lane;
+                kk[u] = vl[u] ? c - rec[u].z : 0u;
+                const uint64_t ca = (((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * kk[u];
+                x[u] = load_nt_global(ca);
+            }
+            if (!side_done) side();
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!gv[u]) break;  // uniform
+                uint4 v = x[u];
+                const uint32_t m = rec[u].w;
+                const uint32_t pn = m & 0xFFu;
+                const bool first = kk[u] == 0u;
+                const bool last = kk[u] + 1u == pn;
+                const uint32_t q = (m >> 18) & 63u;
+                if (vl[u] && first && (m & (1u << 24))) s_edge[2u * q] = x[u];
+                if (vl[u] && last && (m & (1u << 25))) s_edge[2u * q + 1u] = x[u];
+                if (__builtin_amdgcn_ballot_w64((m & (1u << 17)) != 0u)) {
+                    const uint32_t sel = (m & (1u << 17)) ? 0x02030001u : 0x03020100u;
+                    v.x = __builtin_amdgcn_perm(v.x, v.x, sel);
+                    v.y = __builtin_amdgcn_perm(v.y, v.y, sel);
+                    v.z = __builtin_amdgcn_perm(v.z, v.z, sel);
+                    v.w = __builtin_amdgcn_perm(v.w, v.w, sel);
+                }
+                uint32_t val = 0;
+                val = dot2_acc(v.x, val);
+                val = dot2_acc(v.y, val);
+                val = dot2_acc(v.z, val);
+                val = dot2_acc(v.w, val);
+                val = vl[u] ? val : 0u;
+                const uint32_t P = wave_incl_scan(val);
+                const uint32_t add = (first ? val - P : 0u) + ((last || lane == 63u) ? P : 0u);
+                if (vl[u] && (first || last || lane == 63u)) atomicAdd(&s_acc[q], add);
+            }
+        }
+
+        if (!side_done) side();  // a tile with nothing to sweep
+
+        // ---- 3. descriptors longer than WCAP chunks, one wave each
+        uint64_t bigm = __builtin_amdgcn_ballot_w64(big);
+        while (bigm) {
+            const uint32_t q = (uint32_t)__builtin_ctzll(bigm);
+            bigm &= bigm - 1ull;
+            const lvlip_csum_desc d = descs[t * D + q];
+            const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
+            const int lo = (int)(abs & 15ull);
+            const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
+            const uint32_t nchq = (uint32_t)((span + 15u) >> 4);
+            const uint32_t lastv = (uint32_t)(span - 16ull * (nchq - 1u));
+            const uint4* src = reinterpret_cast<const uint4*>(abs & ~15ull);
+            uint32_t w = (abs & 1ull) ? wave_packet_sum<4, true>(src, nchq, lo, lastv, lane)
+                                      : wave_packet_sum<4, false>(src, nchq, lo, lastv, lane);
+            w = wave_sum_dpp(w);
+            if (lane == 0) s_acc[q] = w;
+        }
+        lds_sync();
+
+        // ---- 4. edge corrections (bytes of the first / last chunk outside the
+        // descriptor, once per descriptor, mod 2^32), fold; the store goes out
+        // behind the next tile's first sweep loads
+        uint32_t acc = s_acc[lane < (uint32_t)D ? lane : 0u];
+        if (meta & (3u << 24)) {
+            const bool odd = meta & (1u << 17);
+            const int lo = (int)((meta >> 8) & 15u), lastv = (int)((meta >> 12) & 31u);
+            uint32_t c = 0;
+            if (meta & (1u << 24)) {
+                uint4 f = s_edge[2u * lane];
+                const int fb1 = (nch == 1u) ? lastv : 16;
+                f.x &= ~byte_range_mask(lo, fb1, 0);
+                f.y &= ~byte_range_mask(lo, fb1, 1);
+                f.z &= ~byte_range_mask(lo, fb1, 2);
+                f.w &= ~byte_range_mask(lo, fb1, 3);
+                c += odd ? chunk_words<true>(f) : chunk_words<false>(f);
+            }
+            if (meta & (1u << 25)) {
+                uint4 l = s_edge[2u * lane + 1u];
+                l.x &= ~byte_range_mask(0, lastv, 0);
+                l.y &= ~byte_range_mask(0, lastv, 1);
+                l.z &= ~byte_range_mask(0, lastv, 2);
+                l.w &= ~byte_range_mask(0, lastv, 3);
+                c += odd ? chunk_words<true>(l) : chunk_words<false>(l);
+            }
+            acc -= c;
+        }
+        res_prev = finish(start_sum, acc);
+        i_prev = i;
+        st_prev = mine;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (st_prev) out[i_prev] = res_prev;
+}
+
+}  // namespace lvlip
+
+namespace {
+
+uint32_t grid_for(uint32_t n, uint32_t packets_per_block, int waves_per_cu, int waves_per_block) {
+    uint64_t blocks = ((uint64_t)n + packets_per_block - 1) / packets_per_block;
+    if (waves_per_cu > 0) {
+        const uint64_t cap = (uint64_t)lvlip_host::current_cus() * (uint64_t)waves_per_cu / waves_per_block;
+        if (cap > 0 && blocks > cap) blocks = cap;
+    }
+    if (blocks == 0) blocks = 1;
+    return (uint32_t)blocks;
+}
+
+template <int U>
+void launch_wave_simple(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                        uint32_t n, uint16_t* out) {
+    hipLaunchKernelGGL(lvlip::k_wave_simple<U>, dim3(grid), dim3(256), 0, s,
+                       (const uint8_t*)base, d, n, out);
+}
+
+// Persistent streaming launch: waves_per_cu waves on every CU, each owning a
+// contiguous range of ceil(n / waves) packets.
+// LVLIP_LOAD_POLICY (A/B knob, read once): the data loads' cache
+// policy.  nt (default) | temporal | nt_sc1 | nt_sc0sc1 | sc1; the flat kernel
+// knows nt and temporal only (anything else is nt there).
+int load_policy() {
+    static const int pol = [] {
+        const char* e = getenv("LVLIP_LOAD_POLICY");
+        if (!e) return 0;
+        if (!strcmp(e, "temporal")) return 1;
+        if (!strcmp(e, "nt_sc1")) return 2;
+        if (!strcmp(e, "nt_sc0sc1")) return 3;
+        if (!strcmp(e, "sc1")) return 4;
+        return 0;
+    }();
+    return pol;
+}
+bool load_nt() { return load_policy() != 1; }
+
+// LVLIP_FLAT_GROUPS (A/B knob, read once): k_flat2's group order.
+// block (default, 2: rounds of 4U consecutive groups, U per wave) | quarters
+// (1: contiguous quarters of the tile per wave, round 1's order) | interleaved
+// (0: groups w, w+4, ...; batch calls only).
+int flat_group_order() {
+    static const int c = [] {
+        const char* e = getenv("LVLIP_FLAT_GROUPS");
+        if (e && strcmp(e, "interleaved") == 0) return 0;
+        if (e && strcmp(e, "quarters") == 0) return 1;
+        return 2;
+    }();
+    return c;
+}
+
+// LVLIP_FLAT_LDS_PAD (A/B knob, read once): bytes of unused dynamic LDS per
+// k_flat2 workgroup, which caps the resident workgroups per CU (160 KiB / (19 KiB
+// + pad)); 0 = none.
+size_t flat_lds_pad() {
+    static const size_t v = [] {
+        const char* e = getenv("LVLIP_FLAT_LDS_PAD");
+        const long x = e ? atol(e) : 0;
+        return (size_t)(x < 0 ? 0 : (x > 131072 ? 131072 : x));
+    }();
+    return v;
+}
+
+// k_stream: waves_per_cu waves on every CU (fewer when the batch has fewer
+// packets), whole 256-thread blocks; each wave owns a contiguous range of
+// ceil(n / waves) packets.
+template <int U>
+void launch_stream(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                   uint32_t n, uint16_t* out) {
+    uint64_t waves = (uint64_t)lvlip_host::current_cus() * (uint64_t)waves_per_cu;
+    if (waves > n) waves = n;
+    waves = (waves + 3) & ~3ull;  // whole 256-thread blocks
+    const uint32_t grid = (uint32_t)(waves / 4);
+    switch (load_policy()) {
+#define LVLIP_STREAM_POL(P)                                                              \
+    case P:                                                                              \
+        hipLaunchKernelGGL((lvlip::k_stream<U, P>), dim3(grid), dim3(256), 0, s,         \
+                           (const uint8_t*)base, d, n, out);                             \
+        break;
+        LVLIP_STREAM_POL(1)
+        LVLIP_STREAM_POL(2)
+        LVLIP_STREAM_POL(3)
+        LVLIP_STREAM_POL(4)
+#undef LVLIP_STREAM_POL
+        default:
+            hipLaunchKernelGGL((lvlip::k_stream<U, 0>), dim3(grid), dim3(256), 0, s,
+                               (const uint8_t*)base, d, n, out);
+    }
+}
+
+// k_wflat: waves_per_cu waves on every CU (fewer when the batch has fewer
+// tiles); the grid stays a multiple of 8 blocks when it can (XCD-major ranks).
+template <int U, int D>
+void launch_wflat_ud(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                     uint32_t n, uint16_t* out) {
+    uint64_t waves = (uint64_t)lvlip_host::current_cus() * (uint64_t)waves_per_cu;
+    const uint64_t nt = ((uint64_t)n + D - 1) / D;
+    if (waves > nt) waves = nt;
+    uint64_t grid = (waves + lvlip::SW_WAVES - 1) / lvlip::SW_WAVES;
+    if (grid > 8) grid = grid & ~7ull;
+    hipLaunchKernelGGL((lvlip::k_wflat<U, D>), dim3((uint32_t)grid), dim3(256), 0, s,
+                       (const uint8_t*)base, d, n, out);
+}
+
+template <int U>
+bool launch_wflat(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                  uint32_t n, uint16_t* out, int tile) {
+    switch (tile) {
+        case 16: launch_wflat_ud<U, 16>(waves_per_cu, s, base, d, n, out); return true;
+        case 32: launch_wflat_ud<U, 32>(waves_per_cu, s, base, d, n, out); return true;
+        case 64: launch_wflat_ud<U, 64>(waves_per_cu, s, base, d, n, out); return true;
+        default: return false;
+    }
+}
+
+template <int U>
+void launch_wave_lds(uint32_t grid, hipStream_t s, const void* base, const lvlip_csum_desc* d,
+                     uint32_t n, uint16_t* out) {
+    hipLaunchKernelGGL(lvlip::k_wave_lds<U>, dim3(grid), dim3(256), 0, s,
+                       (const uint8_t*)base, d, n, out);
+}
+
+int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uint16_t* out, hipStream_t s,
+                 const lvlip_launch_cfg* cfg) {
+    const int kernel = cfg ? cfg->kernel : -1;
+    int unroll = cfg ? cfg->unroll : 0;
+    const int wpc = cfg ? cfg->waves_per_cu : 0;
+    switch (kernel) {
+        case 1: {  // k_stream: unroll = 2-KiB pieces in flight per wave
+            if (unroll <= 0) unroll = 2;
+            const int w = wpc > 0 ? wpc : 16;
+            switch (unroll) {
+                case 2: launch_stream<2>(w, s, base, descs, n, out); break;
+                case 3: launch_stream<3>(w, s, base, descs, n, out); break;
+                case 4: launch_stream<4>(w, s, base, descs, n, out); break;
+                default: return LVLIP_EINVAL;
+            }
+            break;
+        }
+        case 9: {  // k_wflat: loads per round | descriptors per tile << 8
+            int u = unroll > 0 ? unroll & 0xff : 0;
+            int tile = unroll > 0 ? (unroll >> 8) & 0xff : 0;
+            if (u == 0) u = 4;
+            if (tile == 0) tile = 32;
+            const int w = wpc > 0 ? wpc : 8;
+            bool ok = false;
+            switch (u) {
+                case 2: ok = launch_wflat<2>(w, s, base, descs, n, out, tile); break;
+                case 4: ok = launch_wflat<4>(w, s, base, descs, n, out, tile); break;
+                case 8: ok = launch_wflat<8>(w, s, base, descs, n, out, tile); break;
+                default: break;
+            }
+            if (!ok) return LVLIP_EINVAL;
+            break;
+        }
+        case 4: {
+            if (unroll <= 0) unroll = 2;
+            const uint32_t grid = grid_for(n, 4, wpc, 4);
+            switch (unroll) {
+                case 1: launch_wave_simple<1>(grid, s, base, descs, n, out); break;
+                case 2: launch_wave_simple<2>(grid, s, base, descs, n, out); break;
+                case 4: launch_wave_simple<4>(grid, s, base, descs, n, out); break;
+                default: return LVLIP_EINVAL;
+            }
+            break;
+        }
+        case 2: {
+            if (unroll <= 0) unroll = 2;
+            const uint32_t grid = grid_for(n, 4, wpc, 4);
+            switch (unroll) {
+                case 1: launch_wave_lds<1>(grid, s, base, descs, n, out); break;
+                case 2: launch_wave_lds<2>(grid, s, base, descs, n, out); break;
+                case 4: launch_wave_lds<4>(grid, s, base, descs, n, out); break;
+                default: return LVLIP_EINVAL;
+            }
+            break;
+        }
+        case 3: {
+            // k_flat2's A/B shapes: loads per round | group order + 1 << 8 (1
+            // interleaved, 2 quarters, 3 blocks; 0 = LVLIP_FLAT_GROUPS, else
+            // blocks) | 1 << 10 for tiles of 512 descriptors (U 4 or 8,
+            // quarters or blocks); LVLIP_LOAD_POLICY=temporal for plain loads
+            const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
+            if (unroll < 0) unroll = 0;
+            if ((unroll >> 11) != 0) return LVLIP_EINVAL;
+            const int uo = (unroll >> 8) & 3;
+            const bool d2 = (unroll >> 10) & 1;
+            unroll &= 0xFF;
+            if (unroll <= 0) unroll = 8;
+            const bool nt = load_nt();
+            const int gord = uo ? uo - 1 : flat_group_order();
+            if (d2) {
+                const uint32_t grid2 = (uint32_t)(((uint64_t)n + 2 * lvlip::FT - 1) / (2 * lvlip::FT));
+                switch (unroll * 8 + gord) {
+#define LVLIP_FLAT_D2(UU, CG)                                                                  \
+    case UU * 8 + CG:                                                                         \
+        hipLaunchKernelGGL((lvlip::k_flat2<UU, true, CG, lvlip::DescSrc, 2>), dim3(grid2),     \
+                           dim3(lvlip::FT), flat_lds_pad(), s, (const uint8_t*)base,         \
+                           lvlip::DescSrc{descs, out}, n);                                  \
+        break;
+                    LVLIP_FLAT_D2(4, 1) LVLIP_FLAT_D2(4, 2) LVLIP_FLAT_D2(8, 1) LVLIP_FLAT_D2(8, 2)
+#undef LVLIP_FLAT_D2
+                    default: return LVLIP_EINVAL;
+                }
+                break;
+            }
+            switch (unroll * 8 + (nt ? 4 : 0) + gord) {
+#define LVLIP_FLAT(UU, NTV, CG)                                                               \
+    case UU * 8 + (NTV ? 4 : 0) + CG:                                                        \
+        hipLaunchKernelGGL((lvlip::k_flat2<UU, NTV, CG, lvlip::DescSrc>), dim3(grid),         \
+                           dim3(lvlip::FT), flat_lds_pad(), s, (const uint8_t*)base,         \
+                           lvlip::DescSrc{descs, out}, n);                                  \
+        break;
+                LVLIP_FLAT(2, true, 1) LVLIP_FLAT(2, true, 0) LVLIP_FLAT(2, true, 2)
+                LVLIP_FLAT(2, false, 1) LVLIP_FLAT(2, false, 0) LVLIP_FLAT(2, false, 2)
+                LVLIP_FLAT(4, true, 1) LVLIP_FLAT(4, true, 0) LVLIP_FLAT(4, true, 2)
+                LVLIP_FLAT(4, false, 1) LVLIP_FLAT(4, false, 0) LVLIP_FLAT(4, false, 2)
+                LVLIP_FLAT(8, true, 1) LVLIP_FLAT(8, true, 0) LVLIP_FLAT(8, true, 2)
+                LVLIP_FLAT(8, false, 1) LVLIP_FLAT(8, false, 0) LVLIP_FLAT(8, false, 2)
+                LVLIP_FLAT(6, true, 1) LVLIP_FLAT(6, true, 2) LVLIP_FLAT(12, true, 1) LVLIP_FLAT(12, true, 2)
+#undef LVLIP_FLAT
+                default: return LVLIP_EINVAL;
+            }
+            break;
+        }
+        case 5: {  // first-generation flat kernel
+            const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FLAT_T - 1) / lvlip::FLAT_T);
+            hipLaunchKernelGGL(lvlip::k_flat, dim3(grid), dim3(lvlip::FLAT_T), 0, s, (const uint8_t*)base, descs,
+                               n, out);
+            break;
+        }
+        default: return LVLIP_EINVAL;
+    }
+    return hipGetLastError() == hipSuccess ? LVLIP_OK : LVLIP_EHIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+// lvlip_csum_batch_dev_ex's contract for the lab kernel ids (1, 2, 3, 4, 5, 9).
+__attribute__((visibility("default"))) int lvlip_lab_batch_dev_ex(const void* base,
+                                                                  const lvlip_csum_desc* descs, uint32_t n,
+                                                                  uint16_t* out, void* stream,
+                                                                  const lvlip_launch_cfg* cfg) {
+    if (n == 0) return LVLIP_OK;
+    if (!base || !descs || !out || n > LVLIP_MAX_BATCH || ((uintptr_t)base & 15u) != 0) return LVLIP_EINVAL;
+    for (uint32_t lo = 0; lo < n;) {
+        const uint32_t m = n - lo < lvlip_host::kLaunchMax ? n - lo : lvlip_host::kLaunchMax;
+        const int rc = lab_dispatch(base, descs + lo, m, out + lo, (hipStream_t)stream, cfg);
+        if (rc != LVLIP_OK) return rc;
+        lo += m;
+    }
+    return LVLIP_OK;
+}
+
+// The frame calls' A/B variants on k_flat2 with a frame source.
+// mode: 0 TX fill, 1 RX header (the flat sweep instead of k_rx_hdr), 2 RX +
+// L4.  variant bits: 1 plain (temporal) TX field stores, 2 eight loads per
+// round, 4 block group order (else quarters).
+__attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int variant, void* base,
+                                                                const lvlip_frame_desc* frames, uint32_t n,
+                                                                uint8_t* out8, void* stream) {
+    if (n == 0) return LVLIP_OK;
+    if (!base || !frames || n > LVLIP_MAX_BATCH / 2u || ((uintptr_t)base & 15u)) return LVLIP_EINVAL;
+    if (mode != 0 && !out8) return LVLIP_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const bool nt = !(variant & 1), u8 = variant & 2, blocks = variant & 4;
+#define LVLIP_LAB_FR(M)                                                                              \
+    (u8 ? (blocks ? lvlip::launch_frames_flat<M, 8, 2>(base, frames, n, out8, s, nt)                \
+                  : lvlip::launch_frames_flat<M, 8, 1>(base, frames, n, out8, s, nt))               \
+        : (blocks ? lvlip::launch_frames_flat<M, 4, 2>(base, frames, n, out8, s, nt)                \
+                  : lvlip::launch_frames_flat<M, 4, 1>(base, frames, n, out8, s, nt)))
+    switch (mode) {
+        case 0: return LVLIP_LAB_FR(lvlip::FR_TX);
+        case 1: return LVLIP_LAB_FR(lvlip::FR_RX);
+        case 2: return LVLIP_LAB_FR(lvlip::FR_RX_L4);
+        default: return LVLIP_EINVAL;
+    }
+#undef LVLIP_LAB_FR
+}
+
+}  // extern "C"

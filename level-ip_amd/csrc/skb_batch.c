@@ -5,6 +5,7 @@
  * batch through lvlip_csum_batch_host (csum_ctx.cpp).
  */
 #include <pthread.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -472,4 +473,103 @@ uint32_t lvlip_icmp_echo_reply_fill(lvlip_frame *frames, uint32_t n)
         memcpy(icmp + 2, &v, 2);
     }
     return recomputed;
+}
+
+/* --------------------------------------------- f1/f2 over level-ip's skb queues */
+
+/* struct sk_buff (include/skbuff.h:9-23) and struct sk_buff_head (:25-29) on
+ * LP64: the intrusive list_head (include/list.h) first, then the fields these
+ * walkers read.  csum_cpu.c pins len and data of the same layout. */
+struct lvlip_skb_layout {
+    struct lvlip_skb_layout *next, *prev; /* struct list_head list */
+    void *rt;
+    void *dev;
+    int refcnt;
+    uint16_t protocol;
+    uint32_t len;
+    uint32_t dlen;
+    uint32_t seq;
+    uint32_t end_seq;
+    uint8_t *end;
+    uint8_t *head;
+    uint8_t *data;
+    uint8_t *payload;
+};
+_Static_assert(offsetof(struct lvlip_skb_layout, len) == 40, "sk_buff.len offset");
+_Static_assert(offsetof(struct lvlip_skb_layout, end) == 56, "sk_buff.end offset");
+_Static_assert(offsetof(struct lvlip_skb_layout, head) == 64, "sk_buff.head offset");
+_Static_assert(offsetof(struct lvlip_skb_layout, data) == 72, "sk_buff.data offset");
+
+struct lvlip_skb_queue_layout {
+    struct lvlip_skb_layout *next, *prev; /* struct list_head head */
+    uint32_t qlen;
+};
+
+/* The queue's skbs in list order as frames (list_for_each, include/list.h).
+ * rx: skb->data .. skb->end; tx: skb->data - ETH_HDR_LEN, skb->len + 14.
+ * Returns the count, or -1 on a malformed entry / allocation failure. */
+static int64_t skb_list_frames(struct sk_buff_head *q, int rx, lvlip_frame **out)
+{
+    struct lvlip_skb_queue_layout *h = (struct lvlip_skb_queue_layout *)(void *)q;
+    const void *stop = h;
+    uint64_t n = 0;
+    for (struct lvlip_skb_layout *s = h->next; (const void *)s != stop; s = s->next) {
+        if (!s || n >= LVLIP_MAX_BATCH / 2u) return -1;
+        n++;
+    }
+    *out = NULL;
+    if (n == 0) return 0;
+    lvlip_frame *f = (lvlip_frame *)malloc(sizeof(lvlip_frame) * (size_t)n);
+    if (!f) return -1;
+    uint64_t k = 0;
+    for (struct lvlip_skb_layout *s = h->next; (const void *)s != stop; s = s->next, k++) {
+        if (rx) {
+            if (!s->data || s->end < s->data) {
+                free(f);
+                return -1;
+            }
+            f[k].head = s->data; /* tun_read's buffer, src/netdev.c:91 */
+            f[k].len = (uint32_t)(s->end - s->data);
+        } else {
+            if (!s->data || s->data - s->head < (ptrdiff_t)ETH_HDR_LEN) {
+                free(f);
+                return -1;
+            }
+            f[k].head = s->data - ETH_HDR_LEN; /* netdev_transmit's push, src/netdev.c:40-61 */
+            f[k].len = s->len + ETH_HDR_LEN;
+        }
+    }
+    *out = f;
+    return (int64_t)n;
+}
+
+int lvlip_rx_verify_skb_list(lvlip_csum_ctx *ctx, struct sk_buff_head *q, uint32_t flags,
+                             uint8_t *verdict, uint32_t cap)
+{
+    if (!ctx || !q) return LVLIP_EINVAL;
+    lvlip_frame *f = NULL;
+    const int64_t n = skb_list_frames(q, 1, &f);
+    if (n < 0) return LVLIP_EINVAL;
+    if ((uint64_t)n > cap) {
+        free(f);
+        return LVLIP_ERANGE;
+    }
+    if (n && !verdict) {
+        free(f);
+        return LVLIP_EINVAL;
+    }
+    const int rc = n ? lvlip_rx_verify(ctx, f, (uint32_t)n, flags, verdict) : LVLIP_OK;
+    free(f);
+    return rc == LVLIP_OK ? (int)n : rc;
+}
+
+int lvlip_tx_checksum_skb_list(lvlip_csum_ctx *ctx, struct sk_buff_head *q)
+{
+    if (!ctx || !q) return LVLIP_EINVAL;
+    lvlip_frame *f = NULL;
+    const int64_t n = skb_list_frames(q, 0, &f);
+    if (n < 0) return LVLIP_EINVAL;
+    const int rc = n ? lvlip_tx_checksum(ctx, f, (uint32_t)n) : LVLIP_OK;
+    free(f);
+    return rc == LVLIP_OK ? (int)n : rc;
 }

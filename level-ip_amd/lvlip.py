@@ -28,12 +28,18 @@ LAB_PATH = os.path.join(HERE, "liblvlip_lab.so")
 
 # error codes (include/lvlip_csum.h)
 OK, EINVAL, ENODEV, EHIP, ENOMEM, ERANGE = 0, -1, -2, -3, -4, -5
-KERNEL_AUTO, KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_FLAT, KERNEL_WAVE_SIMPLE = 0, 1, 2, 3, 4
-KERNEL_WINDOW, KERNEL_WFLAT, KERNEL_LANE = 8, 9, 10  # (6, 7: retired round-1 A/B ids, run WAVE)
+# the product's kernels (include/lvlip_csum.h)
+KERNEL_AUTO, KERNEL_FLAT, KERNEL_WINDOW, KERNEL_LANE = 0, 3, 8, 10
+# the A/B variants measured against them, in liblvlip_lab.so (lab_kernels.hip);
+# batch_dev sends these ids (and FLAT's A/B shapes) there, the product
+# returns EINVAL for them.  6 and 7 are retired round-1 ids (EINVAL everywhere).
+KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_WAVE_SIMPLE, KERNEL_FLAT_V1, KERNEL_WFLAT = 1, 2, 4, 5, 9
+LAB_KERNELS = (KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_WAVE_SIMPLE, KERNEL_FLAT_V1, KERNEL_WFLAT)
 REG_DMA, REG_ZEROCOPY = 0, 1
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "wave_lds": KERNEL_WAVE_LDS,
-                "flat": KERNEL_FLAT, "wave_simple": KERNEL_WAVE_SIMPLE, "flat_v1": 5,
+                "flat": KERNEL_FLAT, "wave_simple": KERNEL_WAVE_SIMPLE, "flat_v1": KERNEL_FLAT_V1,
                 "window": KERNEL_WINDOW, "wflat": KERNEL_WFLAT, "lane": KERNEL_LANE}
+KERNEL_LABELS = {v: k for k, v in KERNEL_NAMES.items()}
 
 # struct lvlip_csum_desc {u64 offset; i32 len; u32 start_sum;}  (16 B)
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<i4"), ("start_sum", "<u4")])
@@ -106,8 +112,33 @@ def _load(path: str) -> ctypes.CDLL:
         raise LvlipUnavailable(f"cannot load {path}: {e}") from e
 
 
+BUILD_SOURCES = os.path.join(HERE, "BUILD_SOURCES")
+
+
+def source_build_id() -> str:
+    """SHA-256 (first 16 hex digits) of the product's sources in the tree, in
+    the order BUILD_SOURCES lists them: what level-ip_amd/Makefile compiles into
+    lvlip_build_id()."""
+    import hashlib
+
+    root = os.path.dirname(HERE)
+    h = hashlib.sha256()
+    with open(BUILD_SOURCES) as f:
+        for rel in f.read().split():
+            with open(os.path.join(root, rel), "rb") as g:
+                h.update(g.read())
+    return h.hexdigest()[:16]
+
+
 _share_torch_hip_runtime()
 _lib = _load(LIB_PATH)
+_lib.lvlip_build_id.restype = ctypes.c_char_p
+_lib.lvlip_build_id.argtypes = []
+BUILD_ID = _lib.lvlip_build_id().decode()
+if BUILD_ID != source_build_id():
+    raise LvlipUnavailable(
+        f"{LIB_PATH} was built from other sources (build id {BUILD_ID}, tree "
+        f"{source_build_id()}): rebuild with `make -C level-ip_amd`")
 
 # every entry point declared in include/lvlip_csum.h, with its ctypes signature
 SIGNATURES = {
@@ -157,6 +188,13 @@ SIGNATURES = {
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "lvlip_pseudo_sum_rfc": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8,
                                                ctypes.c_uint16]),
+    "lvlip_icmp_echo_reply_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                 ctypes.c_void_p, ctypes.c_void_p]),
+    "lvlip_rx_verify_skb_list": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                ctypes.c_void_p, ctypes.c_uint32]),
+    "lvlip_tx_checksum_skb_list": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "lvlip_auto_kernel": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(LaunchCfg)]),
+    "lvlip_build_id": (ctypes.c_char_p, []),
     "lvlip_abi_version": (ctypes.c_int, []),
     "lvlip_device_count": (ctypes.c_int, []),
     "lvlip_last_hip_error": (ctypes.c_char_p, []),
@@ -231,13 +269,38 @@ def ip_send_check(hdr: bytearray) -> None:
 
 # ---------------------------------------------------------- device batches --
 
+def is_lab_kernel(kernel: int, unroll: int = 0) -> bool:
+    """The A/B variants that live in liblvlip_lab.so: the lab kernel ids, and
+    FLAT's shapes other than the product's (2, 4 or 8 loads per round, block
+    order)."""
+    if kernel in LAB_KERNELS:
+        return True
+    return kernel == KERNEL_FLAT and unroll not in (0, 2, 4, 8)
+
+
 def batch_dev(base_ptr: int, desc_ptr: int, n: int, out_ptr: int, stream: int = 0,
               kernel: int = KERNEL_AUTO, unroll: int = 0, waves_per_cu: int = 0,
               len_hint: int = 0) -> None:
-    """lvlip_csum_batch_dev_ex on raw device pointers (async on `stream`)."""
+    """lvlip_csum_batch_dev_ex on raw device pointers (async on `stream`); an
+    A/B variant id goes to lvlip_lab_batch_dev_ex (liblvlip_lab.so) instead."""
     cfg = LaunchCfg(kernel, unroll, waves_per_cu, min(max(int(len_hint), 0), 0x7FFFFFFF))
+    if is_lab_kernel(kernel, unroll):
+        _check(lab().lvlip_lab_batch_dev_ex(base_ptr, desc_ptr, n, out_ptr, stream or None,
+                                            ctypes.byref(cfg)), "lvlip_lab_batch_dev_ex")
+        return
     _check(_lib.lvlip_csum_batch_dev_ex(base_ptr, desc_ptr, n, out_ptr, stream or None,
                                         ctypes.byref(cfg)), "lvlip_csum_batch_dev_ex")
+
+
+def auto_kernel(len_hint: int, n: int) -> LaunchCfg:
+    """The kernel and shape LVLIP_KERNEL_AUTO runs (lvlip_auto_kernel)."""
+    cfg = LaunchCfg()
+    _lib.lvlip_auto_kernel(min(max(int(len_hint), 0), 0x7FFFFFFF), n, ctypes.byref(cfg))
+    return cfg
+
+
+def auto_kernel_name(len_hint: int, n: int) -> str:
+    return KERNEL_LABELS[auto_kernel(len_hint, n).kernel]
 
 
 def batch_torch(base, descs, out=None, kernel: int = KERNEL_AUTO, unroll: int = 0,
@@ -401,6 +464,34 @@ def tx_checksum_dev(base, fdescs, stream=None):
     return status[:n]
 
 
+def icmp_echo_reply_dev(base, fdescs, stream=None):
+    """lvlip_icmp_echo_reply_dev (f4) in place on frames in a CUDA uint8 tensor;
+    returns the per-frame status (1 updated, 2 recomputed, 0 untouched)."""
+    import torch
+
+    n, fd = _frames_dev(base, fdescs)
+    status = torch.empty(max(n, 1), dtype=torch.uint8, device=base.device)
+    s = stream or torch.cuda.current_stream(base.device)
+    _check(_lib.lvlip_icmp_echo_reply_dev(base.data_ptr(), fd.data_ptr(), n, status.data_ptr(),
+                                          s.cuda_stream), "lvlip_icmp_echo_reply_dev")
+    return status[:n]
+
+
+def frames_variant_dev(mode: int, variant: int, base, fdescs, stream=None):
+    """The frame calls' A/B variants (lvlip_lab_frames_dev, liblvlip_lab.so):
+    mode 0 TX fill, 1 RX header on the flat sweep, 2 RX + L4; variant bits 1
+    plain field stores, 2 eight loads per round, 4 block order.  Returns the
+    per-frame status / verdict tensor."""
+    import torch
+
+    n, fd = _frames_dev(base, fdescs)
+    out8 = torch.empty(max(n, 1), dtype=torch.uint8, device=base.device)
+    s = stream or torch.cuda.current_stream(base.device)
+    _check(lab().lvlip_lab_frames_dev(mode, variant, base.data_ptr(), fd.data_ptr(), n, out8.data_ptr(),
+                                      s.cuda_stream), "lvlip_lab_frames_dev")
+    return out8[:n]
+
+
 def icmp_echo_reply_csum(req_csum: int) -> int:
     """f4 (RFC 1624): reply checksum field from a verified request's field, or
     CSUM_RECOMPUTE."""
@@ -527,7 +618,7 @@ _lab = None
 
 
 def lab() -> ctypes.CDLL:
-    """liblvlip_lab.so: read-bandwidth probes (diagnostics only)."""
+    """liblvlip_lab.so: read-bandwidth probes and the A/B kernels (diagnostics only)."""
     global _lab
     if _lab is None:
         lb = _load(LAB_PATH)
@@ -547,6 +638,12 @@ def lab() -> ctypes.CDLL:
         lb.lvlip_lab_probe_chunk.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                              ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_int, ctypes.c_void_p]
+        lb.lvlip_lab_batch_dev_ex.restype = ctypes.c_int
+        lb.lvlip_lab_batch_dev_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(LaunchCfg)]
+        lb.lvlip_lab_frames_dev.restype = ctypes.c_int
+        lb.lvlip_lab_frames_dev.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
         lb.lvlip_lab_probe_pkwin.restype = ctypes.c_int
         lb.lvlip_lab_probe_pkwin.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                              ctypes.c_int, ctypes.c_int, ctypes.c_void_p]

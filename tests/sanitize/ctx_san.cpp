@@ -20,6 +20,8 @@
 #include <thread>
 #include <vector>
 
+#include <sanitizer/allocator_interface.h>
+
 #include "lvlip_csum.h"
 #include "lvlip_skb.h"
 
@@ -186,10 +188,17 @@ int main() {
     }
     printf("ctx_san: all checks passed\n");
     fflush(stdout);
-    // Every context is destroyed and every check has run.  Skip the static
-    // destructors: at exit the HSA runtime frees its own objects after the HIP
-    // runtime is unloaded, and ASan's device allocator then aborts recycling a
-    // quarantined device chunk (sanitizer_allocator_device.h:125, inside
-    // libhsa-runtime64's __cxa_finalize) -- a toolchain teardown order, not this code.
-    _exit(0);
+    // Why the process used to abort at exit (sanitizer_allocator_device.h:125
+    // under libhsa-runtime64's __cxa_finalize): with ASan, hipFree's HSA pool
+    // frees go through ASan's device allocator, which parks every freed device
+    // chunk in the quarantine.  The contexts above freed their arenas there.
+    // During the HSA runtime's own teardown its frees push the quarantine over
+    // its limit, and ASan recycles the oldest parked chunks by calling back
+    // into an HSA runtime that is already half torn down: the CHECK on that
+    // free fails.  Nothing in the library frees device memory from a static
+    // destructor (every context is destroyed explicitly above).  So drain the
+    // quarantine now, while HSA is fully alive: the parked chunks are really
+    // freed here, and the teardown's own frees no longer overflow it.
+    __sanitizer_purge_allocator();
+    return 0;
 }

@@ -32,8 +32,9 @@ def check_line(line: dict, steps: int, warmup: int):
     assert line["scaling"] == "weak" and line["vs_baseline"] is None
     assert line["dtype"] == "u16"
     assert "workload" in line["config"] and "model" not in line["config"]
-    # bench.py checks the sampled outputs against the reference in its cpu_baseline leg
-    assert line["verified_bit_exact"] is (True if line.get("cpu_baseline") else None)
+    # every output of the timed batch checked against the reference (round 3 on;
+    # round 2's lines checked a side sample in the cpu_baseline leg)
+    assert line["verified_bit_exact"] is True
     r = line["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=2e-3)
@@ -106,6 +107,84 @@ def test_committed_trace_matches_bench_line(wl):
     assert int(ks["Calls"]) >= 251 + 8
     avg_ms = float(ks["AverageNs"]) * 1e-6
     assert avg_ms == pytest.approx(line["roofline"]["kernel_ms"], rel=0.03)
+
+
+def _bench(args, env_extra=None, timeout=110):
+    env = dict(os.environ, **(env_extra or {}))
+    env.pop("WORLD_SIZE", None) if "WORLD_SIZE" not in (env_extra or {}) else None
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_self_launch_two_ranks_dry_run():
+    """`bench.py --gpus 2` with no torch.distributed launcher starts its two
+    ranks itself (gloo rehearsal on the CPU: --dry-run does every step but the
+    GPU work) and rank 0 prints one line for the job, naming the world, the
+    backend and who launched the ranks."""
+    out = _bench(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1", "--settle-ms", "0"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["dry_run"] is True and line["value"] is None
+    assert line["n_gpus"] == 2
+    d = line["dist"]
+    assert d["world_size"] == 2 and d["backend"] == "gloo" and d["launcher"] == "bench.py"
+    assert [r["rank"] for r in d["ranks"]] == [0, 1]
+    assert line["cpu_baseline"] is None
+
+
+def test_bench_world_mismatch_fails():
+    """WORLD_SIZE from a launcher that disagrees with --gpus is an error."""
+    out = _bench(["--gpus", "3", "--dry-run", "--steps", "1", "--warmup", "0"],
+                 {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert out.returncode != 0
+    assert "WORLD_SIZE=2" in out.stderr
+
+
+def test_bench_rccl_ranks_need_their_own_gpus():
+    """Under RCCL (the default backend) N ranks need N visible GPUs: on a box
+    with fewer (this container has none) `bench.py --gpus 2` exits non-zero
+    instead of timing one GPU twice."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("enough GPUs here")
+    out = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--settle-ms", "0"])
+    assert out.returncode != 0
+    assert "GPU" in out.stderr or "HIP device" in out.stderr
+
+
+@pytest.mark.gpu
+def test_bench_self_launch_rccl_refuses_one_gpu():
+    """On the one-GPU box: two RCCL ranks cannot each own a GPU, so the run
+    fails loudly (no line, non-zero status)."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one GPU visible")
+    out = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--settle-ms", "0"])
+    assert out.returncode != 0
+    assert "need 2 GPUs" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.gpu
+def test_bench_self_launch_gloo_two_ranks_on_one_gpu():
+    """`bench.py --gpus 2` launching its own two ranks, rehearsed over gloo on
+    the one GPU: one line, n_gpus 2, both ranks' whole timed batches verified
+    against the reference, shared_devices reported."""
+    out = _bench(["--gpus", "2", "--steps", "5", "--warmup", "2", "--packets", "262144",
+                  "--settle-ms", "50"], {"LVLIP_DIST_BACKEND": "gloo"})
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["dist"]["launcher"] == "bench.py"
+    assert line["dist"]["shared_devices"] is True
+    assert line["verified_bit_exact"] is True
+    assert all(r["verified"] for r in line["dist"]["ranks"])
+    assert line["roofline"]["frac_aggregate"] == pytest.approx(line["value"] / 16000.0, rel=1e-3)
 
 
 @pytest.mark.gpu

@@ -417,6 +417,28 @@ def test_bad_launch_shapes_rejected():
             lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None, k, u, 0, 0)
 
 
+def test_retired_and_lab_ids_rejected_by_the_product():
+    """The product library runs AUTO, FLAT (2, 4, 8 loads per round), WINDOW and
+    LANE only: the retired round-1 ids 6 and 7 and the lab's A/B ids return
+    LVLIP_EINVAL there (nothing launched), with no silent substitute."""
+    import ctypes
+
+    base = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    descs = dev_descs(mk_descs([0], [4], [0]))
+    out = torch.empty(1, dtype=torch.int16, device="cuda")
+    L = lvlip.lib()
+    for k, u in ((6, 0), (7, 0), (lvlip.KERNEL_WAVE, 2), (lvlip.KERNEL_WAVE_LDS, 2),
+                 (lvlip.KERNEL_WAVE_SIMPLE, 2), (lvlip.KERNEL_FLAT_V1, 0), (lvlip.KERNEL_WFLAT, 0),
+                 (lvlip.KERNEL_FLAT, 6), (lvlip.KERNEL_FLAT, 4 | (2 << 8))):
+        cfg = lvlip.LaunchCfg(k, u, 0, 0)
+        assert L.lvlip_csum_batch_dev_ex(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None,
+                                         ctypes.byref(cfg)) == lvlip.EINVAL, (k, u)
+    for k in (6, 7):
+        cfg = lvlip.LaunchCfg(k, 0, 0, 0)
+        assert lvlip.lab().lvlip_lab_batch_dev_ex(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(),
+                                                  None, ctypes.byref(cfg)) == lvlip.EINVAL, k
+
+
 # ----------------------------------------------------------- host batches --
 
 def test_host_iov_ragged_unaligned():

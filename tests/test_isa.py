@@ -1,7 +1,8 @@
 """ISA guards for the stream kernels (CPU-only: hipcc cross-compiles gfx950).
 
-The stream kernels rely on hand-placed inline asm (csum_kernels.hip, k_stream and
-k_window, which shares its ring):
+The stream kernels rely on hand-placed inline asm (the ring of csum_dev.h, run
+by k_window in the product, csum_kernels.hip, and by k_stream in the lab
+library, lab_kernels.hip):
   * buffer_load_dwordx4 whose resource words come from v_readfirstlane, a VALU
     write of SGPRs: a VMEM read of them needs 5 wait states (s_nop 4), which
     hipcc does not insert around inline asm;
@@ -18,7 +19,7 @@ import tempfile
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "level-ip_amd", "csrc", "csum_kernels.hip")
+SRCS = [os.path.join(ROOT, "level-ip_amd", "csrc", f) for f in ("csum_kernels.hip", "lab_kernels.hip")]
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
@@ -26,12 +27,15 @@ HIPCC = "/opt/rocm/bin/hipcc"
 def asm():
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
+    text = []
     with tempfile.TemporaryDirectory() as d:
-        out = os.path.join(d, "k.s")
-        subprocess.run([HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17",
-                        "-I" + os.path.join(ROOT, "include"), "-S", "--cuda-device-only",
-                        SRC, "-o", out], check=True, capture_output=True)
-        return open(out).read()
+        for i, src in enumerate(SRCS):
+            out = os.path.join(d, f"k{i}.s")
+            subprocess.run([HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17",
+                            "-I" + os.path.join(ROOT, "include"), "-S", "--cuda-device-only",
+                            src, "-o", out], check=True, capture_output=True)
+            text.append(open(out).read())
+    return "\n".join(text)
 
 
 def functions(text):

@@ -169,19 +169,23 @@ def test_tx_checksum_dev_matches_reference_tx():
     assert np.array_equal(out[mask], buf[mask])
 
 
-def test_tx_checksum_dev_plain_and_nt_stores_agree(monkeypatch):
-    """The device TX fill with both field-store kinds (nontemporal, the default;
-    LVLIP_FRAMES_TX_STORE=plain): identical frames, equal to the oracle's fill,
-    odd and even field addresses (frames at every alignment)."""
+def test_tx_checksum_dev_plain_and_nt_stores_agree():
+    """The device TX fill with both field-store kinds (nontemporal, the product;
+    plain stores, the lab variant) and the lab's other shapes (8 loads per
+    round, block order): identical frames, equal to the oracle's fill, odd and
+    even field addresses (frames at every alignment)."""
     fr = workloads.frames(3000, seed=58) + workloads.frames(100, seed=59, max_l4=8900)
     want = [bytearray(f) for f in fr]
     for f in want:
         skb_oracle.tx_fill(f)
     buf, fd = lvlip.pack_frames(fr, align_mod=16, seed=5)
-    for kind in ("nt", "plain"):
-        monkeypatch.setenv("LVLIP_FRAMES_TX_STORE", kind)
+    for kind in ("nt", "plain", 2, 4, 7):
         base = _dev(buf)
-        assert int(lvlip.tx_checksum_dev(base, fd).sum()) == len(fr), kind
+        if kind == "nt":
+            st = lvlip.tx_checksum_dev(base, fd)
+        else:
+            st = lvlip.frames_variant_dev(0, 1 if kind == "plain" else kind, base, fd)
+        assert int(st.sum()) == len(fr), kind
         out = base.cpu().numpy()
         got = [out[int(d["offset"]):int(d["offset"]) + int(d["len"])].tobytes() for d in fd]
         assert got == [bytes(f) for f in want], kind
@@ -253,9 +257,10 @@ def test_rx_verify_agrees_with_reference_ip_rcv(ctx):
                                                         if v == lvlip.RX_OK]
 
 
-def test_rx_header_lane_and_flat_agree(monkeypatch):
+def test_rx_header_lane_and_flat_agree():
     """The header-only RX call on both of its kernels (k_rx_hdr, one lane per
-    frame, the default; k_flat2 with a frame source, LVLIP_FRAMES_RX_HDR=flat):
+    frame, the product; k_flat2 with a frame source, the lab variant, in its
+    shapes):
     20 000 frames at every alignment, 20 % with IP options (ihl 6-15, the
     window's last words and the byte-load tail), a tenth with a flipped bit in
     the header or beyond, some truncated; every verdict == the oracle's."""
@@ -272,9 +277,153 @@ def test_rx_header_lane_and_flat_agree(monkeypatch):
     want = [skb_oracle.rx_verdict(f, 0) for f in fr]
     buf, fd = lvlip.pack_frames(fr, align_mod=16, seed=4)
     base = _dev(buf)
-    for kern in ("lane", "flat"):
-        monkeypatch.setenv("LVLIP_FRAMES_RX_HDR", kern)
-        got = lvlip.rx_verify_dev(base, fd, 0).cpu().numpy()
+    for kern in ("lane", 0, 2, 4, 6):
+        if kern == "lane":
+            got = lvlip.rx_verify_dev(base, fd, 0).cpu().numpy()
+        else:
+            got = lvlip.frames_variant_dev(1, kern, base, fd).cpu().numpy()
         bad = np.nonzero(got != np.array(want, dtype=np.uint8))[0]
         assert bad.size == 0, (kern, bad[:5])
     assert len(set(want)) >= 3
+
+
+# ------------------------------------------------ f4: echo reply in HBM --
+
+def _icmp_reply_ref(frame: bytes) -> bytes:
+    """icmpv4_reply's ICMP part (src/icmpv4.c:44-47) on a request frame: type 0,
+    checksum field zeroed, checksum over icmp_len = ip.len - ihl*4 bytes (the
+    oracle restatement of src/utils.c:40-55), stored raw."""
+    import pyoracle
+
+    f = bytearray(frame)
+    ihl = f[14] & 0xF
+    l4, n = 14 + ihl * 4, int.from_bytes(f[16:18], "big") - ihl * 4
+    f[l4] = 0
+    f[l4 + 2:l4 + 4] = b"\x00\x00"
+    f[l4 + 2:l4 + 4] = pyoracle.checksum(bytes(f[l4:l4 + n]), n, 0).to_bytes(2, "little")
+    return bytes(f)
+
+
+def _echo_requests(rng, n, ihl_max=5):
+    """n verified ICMP echo requests (random payload lengths, odd ones
+    included) with the RFC 1624 corner cases mixed in: request checksum field
+    0xffff (the other zero: the message sums to 0xffff), and the undecidable
+    replies (S' = 0xffff: an all-zero echo body, whose reply field is 0xffff,
+    and an all-0xff body, whose reply field is 0x0000)."""
+    import pyoracle
+
+    out, kinds = [], []
+    for i in range(n):
+        kind = ("random", "random", "random", "ffff", "zero", "ones")[int(rng.integers(0, 6))] \
+            if i >= 4 else ("ffff", "zero", "ones", "random")[i]
+        ihl = 5 if ihl_max == 5 or rng.random() < 0.5 else int(rng.integers(6, ihl_max + 1))
+        plen = int(rng.integers(0, 1473 - 4 * (ihl - 5)))
+        if kind == "ones":
+            plen &= ~1
+        body = bytearray(4 + plen)  # id, seq, payload
+        if kind == "random" or kind == "ffff":
+            body[:] = rng.integers(0, 256, len(body), dtype=np.uint8).tobytes()
+        elif kind == "ones":
+            body[:] = b"\xff" * len(body)
+        icmp = bytearray(b"\x08\x00\x00\x00") + body
+        if kind == "ffff":
+            # make the message (field zeroed) sum to 0xffff: fix the id word
+            icmp[4:6] = b"\x00\x00"
+            s = 0xFFFF & ~pyoracle.checksum(bytes(icmp), len(icmp), 0)  # one's-complement sum
+            w = (0xFFFF - s) & 0xFFFF  # s + w == 0xffff (one's complement)
+            icmp[4:6] = w.to_bytes(2, "little")
+        c = pyoracle.checksum(bytes(icmp), len(icmp), 0)
+        icmp[2:4] = c.to_bytes(2, "little")
+        if kind == "ffff":
+            assert c == 0
+            icmp[2:4] = b"\xff\xff"  # the other representation, still verifies
+        assert pyoracle.checksum(bytes(icmp), len(icmp), 0) == 0, kind
+        iplen = ihl * 4 + len(icmp)
+        ih = bytearray(rng.integers(0, 256, ihl * 4, dtype=np.uint8).tobytes())
+        ih[0] = 0x40 | ihl
+        ih[2:4] = iplen.to_bytes(2, "big")
+        ih[8] = 64
+        ih[9] = 1
+        pad = bytes(rng.integers(0, 256, int(rng.integers(0, 4)), dtype=np.uint8).tobytes())
+        eth = bytes(rng.integers(0, 256, 12, dtype=np.uint8).tobytes()) + b"\x08\x00"
+        out.append(bytearray(eth + bytes(ih) + bytes(icmp) + pad))
+        kinds.append(kind)
+    return out, kinds
+
+
+def _run_echo_dev(frames):
+    buf, fd = lvlip.pack_frames(frames, align_mod=16, seed=9)
+    base = _dev(buf)
+    st = lvlip.icmp_echo_reply_dev(base, fd).cpu().numpy()
+    out = base.cpu().numpy()
+    got = [out[int(d["offset"]):int(d["offset"]) + int(d["len"])].tobytes() for d in fd]
+    rest = np.ones(buf.size, dtype=bool)
+    for d in fd:
+        rest[int(d["offset"]):int(d["offset"]) + int(d["len"])] = False
+    assert np.array_equal(out[rest], buf[rest])  # nothing outside the frames written
+    return st, got
+
+
+def test_icmp_echo_reply_dev_golden_echo():
+    """Config #1's echo requests (tests/golden/echo.json, recorded from the
+    reference stack): the device reply's ICMP part equals the reference stack's
+    own reply byte for byte."""
+    e = golden_io.echo()["echo"]
+    reqs = [bytearray(bytes.fromhex(c["request_hex"])) for c in e]
+    st, got = _run_echo_dev(reqs)
+    for c, g, s in zip(e, got, st):
+        rep = bytes.fromhex(c["reply_hex"])
+        ihl = g[14] & 0xF
+        n = int.from_bytes(g[16:18], "big") - ihl * 4
+        assert g[34:34 + n] == rep[34:34 + n]
+        assert s in (1, 2)
+
+
+def test_icmp_echo_reply_dev_random_and_corner_cases():
+    """20 000 verified requests (ihl 5-15: the parse window's field and the byte
+    loads past it) plus non-requests (replies, other ICMP types, TCP, short
+    frames): every frame equals the oracle's icmpv4_reply recomputation, the
+    corner fields included; the status says which lanes recomputed."""
+    rng = np.random.default_rng(71)
+    fr, kinds = _echo_requests(rng, 20000, ihl_max=15)
+    others = workloads.frames(600, seed=72)  # TCP and ICMP type 8 with garbage fields
+    for f in others:
+        if f[23] == 1:
+            f[14 + (f[14] & 0xF) * 4] = int(rng.choice([0, 3, 11]))  # not a request
+    short = [bytearray(f[:int(rng.integers(0, 40))]) for f in fr[:50]]
+    allf = fr + others + short
+    st, got = _run_echo_dev(allf)
+    for i, (f, g) in enumerate(zip(fr, got)):
+        assert g == _icmp_reply_ref(f), (i, kinds[i])
+    st_req = st[:len(fr)]
+    und = np.array([k in ("zero", "ones") for k in kinds])
+    assert (st_req[und] == 2).all() and (st_req[~und] == 1).all()
+    for f, g, s in zip(others + short, got[len(fr):], st[len(fr):]):
+        assert s == 0 and g == bytes(f)
+    assert {"ffff", "zero", "ones"} <= set(kinds)
+
+
+@pytest.mark.skipif(not os.path.exists(ref_rx_cases.REF_SO), reason="oracle/_ref/libref.so not built")
+def test_icmp_echo_reply_dev_agrees_with_reference_stack():
+    """2 000 random requests (ihl 5, as icmpv4_reply assumes: it reads the ICMP
+    message at head + 34, src/icmpv4.c:38-43) through level-ip's own ip_rcv ->
+    icmpv4_reply (oracle/_ref/libref.so): the device reply's ICMP part equals
+    the stack's reply for every one, the 0xffff and undecidable fields
+    included."""
+    rng = np.random.default_rng(73)
+    fr, kinds = _echo_requests(rng, 2000)
+    for f in fr:  # the stack checks the IPv4 header and answers 10.0.0.4 only
+        f[14 + 12:14 + 16] = bytes([10, 0, 0, 5])
+        f[14 + 16:14 + 20] = bytes([10, 0, 0, 4])
+        f[14 + 6:14 + 8] = b"\x40\x00"
+        f[14 + 10:14 + 12] = b"\x00\x00"
+        c = lvlip.checksum(bytes(f[14:34]), 20, 0)
+        f[24:26] = c.to_bytes(2, "little")
+        f[0:6] = bytes.fromhex("000c296d5025")
+    replies = ref_rx_cases.reference_replies(fr)
+    st, got = _run_echo_dev(fr)
+    assert all(r is not None for r in replies)
+    for i, (g, r) in enumerate(zip(got, replies)):
+        n = int.from_bytes(g[16:18], "big") - 20
+        assert g[34:34 + n] == r[34:34 + n], (i, kinds[i])
+    assert {"ffff", "zero", "ones"} <= set(kinds)
