@@ -153,6 +153,16 @@ def host_cpus() -> dict:
             "cpu_model": _cpu_model()}
 
 
+def usable_cpus(cpus: dict) -> int:
+    """The CPUs this process may use: its affinity mask, limited by the cgroup
+    CPU quota when one is set (the GPU box: 256 CPUs in the mask, a 16-CPU
+    quota, where 256 threads run slower than 16)."""
+    n = cpus["nproc"]
+    if cpus["cgroup_cpu_quota"]:
+        n = max(1, min(n, int(cpus["cgroup_cpu_quota"] + 0.999)))
+    return n
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -238,10 +248,11 @@ def cpu_baseline(b, first, cpus: dict, budget_s: float = 1.0):
             if dt >= budget:
                 return nb * reps / dt / 1e9, reps, dt
 
-    cores = cpus["nproc"]
+    cores = usable_cpus(cpus)
     allc, reps, dt = rate(host, d, cores, nbytes, budget_s, opt=0, use_reference=use_ref)
-    t16 = min(16, cores)
-    g16 = rate(host, d, t16, nbytes, budget_s, opt=0, use_reference=use_ref)[0]
+    aff = None
+    if cpus["nproc"] != cores:
+        aff = rate(host, d, cpus["nproc"], nbytes, budget_s, opt=0, use_reference=use_ref)[0]
     # one-core figures on a sample (the same packets' first descriptors)
     ns = min(d.size, 131072)
     sd = d[:ns].copy()
@@ -255,11 +266,12 @@ def cpu_baseline(b, first, cpus: dict, budget_s: float = 1.0):
         "value": round(allc, 3), "unit": "GB/s", "cores": cores, "kind": kind,
         "sample": (f"{d.size} descriptors / {nbytes / 1e6:.1f} MB of the timed {b.name} batch, "
                    f"copied back from HBM; {reps} passes in {dt:.2f} s on {cores} threads "
-                   f"(pthreads over contiguous packet ranges, every CPU of the affinity mask); "
+                   f"(pthreads over contiguous packet ranges, one per usable CPU: the affinity mask "
+                   f"of {cpus['nproc']} CPUs under a cgroup quota of {cpus['cgroup_cpu_quota']}); "
                    f"level-ip {'src/utils.c compiled -O0 as its Makefile builds it' if use_ref else 'oracle restatement -O0'}"),
         "nproc": cpus["nproc"], "cores_used": cores, "machine_cpus": cpus["machine_cpus"],
         "cgroup_cpu_quota": cpus["cgroup_cpu_quota"], "cpu_model": cpus["cpu_model"],
-        "threads16_GBps": round(g16, 3),
+        "affinity_threads_GBps": None if aff is None else round(aff, 3),
         "one_core_GBps": round(one, 3),
         "one_core_O2_restatement_GBps": round(o2, 3),
         "dropin_one_core_GBps": round(dropin, 3),
@@ -501,7 +513,7 @@ def run(args, world: int):
     cpus = host_cpus()
     verify, first_chunk = None, None
     if not args.no_verify and not args.dry_run:
-        thr = max(1, cpus["nproc"] // max(1, local_world))
+        thr = max(1, usable_cpus(cpus) // max(1, local_world))
         verify, first_chunk = verify_timed_batch(
             b, base, out, thr, keep_first=(rank == 0 and world == 1 and not args.no_cpu_baseline))
         if not verify["ok"]:

@@ -573,6 +573,15 @@ __device__ __forceinline__ void block_excl_scan2(uint32_t a, uint32_t b, uint32_
     *tb = ab;
 }
 
+// Orders this wave's LDS traffic across lanes (a lane reading what another
+// lane wrote): LDS ops of one wave execute in order, so the compiler only has
+// to be kept from moving them, and the counter drained.  No vmcnt: global
+// loads in flight stay in flight.
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // byte mask of bytes [b0, b1) of a 16-B chunk that fall in dword j
 __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
     const int s = min(max(b0 - 4 * j, 0), 4);

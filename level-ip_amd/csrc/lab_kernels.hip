@@ -286,15 +286,6 @@ struct WflatLds {
     uint4 edge[SW_WAVES][2 * D];            // by descriptor: raw first / last chunk
 };
 
-// Orders this wave's LDS traffic across lanes (a lane reading what another
-// lane wrote): LDS ops of one wave execute in order, so the compiler only has
-// to be kept from moving them, and the counter drained.  No vmcnt: global
-// loads in flight stay in flight.
-__device__ __forceinline__ void lds_sync() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-}
-
 template <int U, int D>
 __global__ __launch_bounds__(256) void k_wflat(const uint8_t* __restrict__ base,
                                                const lvlip_csum_desc* __restrict__ descs,

@@ -29,7 +29,7 @@ LAB_PATH = os.path.join(HERE, "liblvlip_lab.so")
 # error codes (include/lvlip_csum.h)
 OK, EINVAL, ENODEV, EHIP, ENOMEM, ERANGE = 0, -1, -2, -3, -4, -5
 # the product's kernels (include/lvlip_csum.h)
-KERNEL_AUTO, KERNEL_FLAT, KERNEL_WINDOW, KERNEL_LANE = 0, 3, 8, 10
+KERNEL_AUTO, KERNEL_FLAT, KERNEL_WINDOW, KERNEL_LANE, KERNEL_RFLAT = 0, 3, 8, 10, 11
 # the A/B variants measured against them, in liblvlip_lab.so (lab_kernels.hip);
 # batch_dev sends these ids (and FLAT's A/B shapes) there, the product
 # returns EINVAL for them.  6 and 7 are retired round-1 ids (EINVAL everywhere).
@@ -38,7 +38,8 @@ LAB_KERNELS = (KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_WAVE_SIMPLE, KERNEL_FLAT_V1,
 REG_DMA, REG_ZEROCOPY = 0, 1
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "wave_lds": KERNEL_WAVE_LDS,
                 "flat": KERNEL_FLAT, "wave_simple": KERNEL_WAVE_SIMPLE, "flat_v1": KERNEL_FLAT_V1,
-                "window": KERNEL_WINDOW, "wflat": KERNEL_WFLAT, "lane": KERNEL_LANE}
+                "window": KERNEL_WINDOW, "wflat": KERNEL_WFLAT, "lane": KERNEL_LANE,
+                "rflat": KERNEL_RFLAT}
 KERNEL_LABELS = {v: k for k, v in KERNEL_NAMES.items()}
 
 # struct lvlip_csum_desc {u64 offset; i32 len; u32 start_sum;}  (16 B)

@@ -56,6 +56,10 @@ VARIANTS = [
     (lvlip.KERNEL_LANE, 2 | (6 << 8) | (1 << 16), 0),
     (lvlip.KERNEL_LANE, 8 | (1 << 8) | (4 << 16), 0),
     (lvlip.KERNEL_LANE, 4 | (2 << 8) | (8 << 16), 0),
+    (lvlip.KERNEL_RFLAT, 0, 0),    # flat sweep per wave, tiles dealt round robin, ring
+    (lvlip.KERNEL_RFLAT, 2 | (32 << 8), 1),
+    (lvlip.KERNEL_RFLAT, 8 | (64 << 8), 16),
+    (lvlip.KERNEL_RFLAT, 6 | (16 << 8), 4),
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
@@ -228,6 +232,7 @@ def test_full_size_bit_exact(name):
     for variant in [(lvlip.KERNEL_WAVE, 4, 0), (lvlip.KERNEL_WAVE, 3, 4),
                     (lvlip.KERNEL_WINDOW, 3, 0), (lvlip.KERNEL_WINDOW, 2, 0),
                     (lvlip.KERNEL_WFLAT, 0, 0), (lvlip.KERNEL_WFLAT, 8 | (64 << 8), 16),
+                    (lvlip.KERNEL_RFLAT, 0, 0), (lvlip.KERNEL_RFLAT, 8 | (32 << 8), 8),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
                     (lvlip.KERNEL_FLAT, 8 | (1 << 10), 0),
@@ -294,6 +299,32 @@ def test_wflat_tiles(tile):
             got = out.cpu().numpy().view(np.uint16)
             bad = np.nonzero(got != want[:n])[0]
             assert bad.size == 0, (n, u, wpc, bad[:5])
+
+
+# k_rflat: every built (group loads per round, descriptors per tile)
+RFLAT_SHAPES = [(2, 16), (4, 16), (6, 16), (8, 16), (2, 32), (4, 32), (6, 32), (8, 32), (4, 64), (8, 64)]
+
+
+@pytest.mark.parametrize("shape", RFLAT_SHAPES, ids=[f"u{u}d{d}" for u, d in RFLAT_SHAPES])
+def test_rflat_tiles(shape):
+    """k_rflat for every built shape: batch sizes that leave the last tile short
+    or give waves no tile, 1 and 24 waves/CU (long per-wave tile sequences, many
+    waves with one tile), ragged lengths with descriptors past the sweep cap
+    (64 KiB), empty and negative lengths at odd offsets; and batches of tiny
+    packets, whose one-group tiles run the issue side against its limit of
+    tile buffers; every output against the oracle."""
+    u, tile = shape
+    for seed, (base, d, want) in ((200 + u + tile, ragged_batch(200 + u + tile)),
+                                  (300 + u + tile, tiny_batch(300 + u + tile))):
+        for n in BATCH_SIZES:
+            descs = dev_descs(d[:n])
+            for wpc in (0, 1, 24):
+                out = lvlip.batch_torch(base, descs, kernel=lvlip.KERNEL_RFLAT, unroll=u | (tile << 8),
+                                        waves_per_cu=wpc)
+                torch.cuda.synchronize()
+                got = out.cpu().numpy().view(np.uint16)
+                bad = np.nonzero(got != want[:n])[0]
+                assert bad.size == 0, (seed, n, wpc, bad[:5])
 
 
 # (lanes per packet S, packets per group P, chunks per lane K): every built shape
@@ -412,7 +443,9 @@ def test_bad_launch_shapes_rejected():
                  (lvlip.KERNEL_WINDOW, 2 | (5 << 8)), (lvlip.KERNEL_WFLAT, 8 | (48 << 8)),
                  (lvlip.KERNEL_LANE, 3), (lvlip.KERNEL_LANE, 4 | (5 << 8)),
                  (lvlip.KERNEL_LANE, 4 | (1 << 8) | (3 << 16)),
-                 (lvlip.KERNEL_LANE, 4 | (1 << 8) | (1 << 25))):
+                 (lvlip.KERNEL_LANE, 4 | (1 << 8) | (1 << 25)),
+                 (lvlip.KERNEL_RFLAT, 3), (lvlip.KERNEL_RFLAT, 2 | (64 << 8)), (lvlip.KERNEL_RFLAT, 4 | (48 << 8)),
+                 (lvlip.KERNEL_RFLAT, 4 | (1 << 16))):
         with pytest.raises(lvlip.LvlipError):
             lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None, k, u, 0, 0)
 
@@ -678,6 +711,7 @@ def test_max_int_packet():
     for variant in [(lvlip.KERNEL_AUTO, 0, 0), (lvlip.KERNEL_WAVE, 2, 0), (lvlip.KERNEL_FLAT, 0, 0),
                     (lvlip.KERNEL_FLAT, 4 | (2 << 8), 0), (lvlip.KERNEL_WINDOW, 2 | (3 << 8), 0),
                     (lvlip.KERNEL_WINDOW, 3 | (1 << 8), 1), (lvlip.KERNEL_WFLAT, 0, 0),
+                    (lvlip.KERNEL_RFLAT, 0, 0),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_LANE, 0, 0), (lvlip.KERNEL_LANE, 2 | (4 << 8) | (1 << 16), 0)]:
         assert list(run(base, descs, variant)) == list(want), variant
