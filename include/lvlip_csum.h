@@ -122,7 +122,7 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
 /* Kernel selection for lvlip_csum_batch_dev_ex.  AUTO picks by len_hint:
  * >= 896 B -> WINDOW (shape by the hint); 1-32 B -> LANE; otherwise or
  * unknown -> FLAT (measured: DESIGN.md §4-5).  lvlip_auto_kernel() tells
- * which kernel and shape AUTO runs.  Ids 1, 2, 4, 5, 6, 7 and 9 are the A/B
+ * which kernel and shape AUTO runs.  Ids 1, 2, 4, 5, 6, 7, 9 and 11 are the A/B
  * variants measured against these (liblvlip_lab.so, not this library): here
  * they return LVLIP_EINVAL. */
 #define LVLIP_KERNEL_AUTO        0  /* the default                                 */
@@ -133,9 +133,6 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
                                        flight)                                 */
 #define LVLIP_KERNEL_LANE       10  /* a few lanes per packet, chunks summed in
                                        registers (batches of small packets)   */
-#define LVLIP_KERNEL_RFLAT      11  /* FLAT's chunk sweep one wave per tile of
-                                       descriptors, tiles dealt round robin, a
-                                       ring of group loads across tiles       */
 
 typedef struct lvlip_launch_cfg {
     int32_t  kernel;        /* LVLIP_KERNEL_*                               */
@@ -143,16 +140,12 @@ typedef struct lvlip_launch_cfg {
                                per wave (2, 3, 4) | packets per group << 8
                                (1, 2, 3, 4 or 8; 0 = by len_hint);
                                FLAT: 64-chunk loads per round (2, 4, 8);
-                               RFLAT: 64-chunk loads per round (2, 4, 6,
-                               8; 0 = 4) | descriptors per tile << 8 (16,
-                               32, 64; 0 = 16);
                                LANE: packets per lane group | 16-B chunks
                                per lane << 8 | lanes per packet << 16 (1, 2,
                                4, 8) | unconditional loads << 24; longer
                                packets go to a whole-wave loop (0 = 4 | 2 << 8
                                | 2 << 16)                                   */
-    int32_t  waves_per_cu;  /* WINDOW, RFLAT: resident waves per CU (0 = 8,
-                               12)                                          */
+    int32_t  waves_per_cu;  /* WINDOW: resident waves per CU (0 = 8)        */
     int32_t  len_hint;      /* average packet length in bytes if the caller
                                knows it (AUTO uses it), 0 = unknown         */
 } lvlip_launch_cfg;

@@ -218,385 +218,6 @@ __global__ __launch_bounds__(256) void k_rx_hdr(const uint8_t* __restrict__ base
     verdict[f] = (uint8_t)v;
 }
 
-// ------------------------------------------------ k_rflat (ragged, ring) --
-//
-// k_flat2's chunk sweep (csum_dev.h) with k_window's two remedies for the
-// mixed config's gap to the memory system:
-//   * a narrow window: tiles of D descriptors (~6 KB of a mixed batch at
-//     D = 16) dealt round robin over the persistent waves (XCD-major ranks),
-//     so the waves in flight read one window of nw x D descriptors that slides
-//     through the batch, instead of ~1 300 resident workgroups each sweeping
-//     its own ~100 KB tile;
-//   * a ring across tiles: every wave keeps two rounds of U 1-KiB group loads
-//     in flight (round k+1 is issued before round k is reduced), and a tile's
-//     plan (one wave-level scan, records and head bitmaps in the wave's LDS)
-//     is made while the previous tile's loads are in flight.  k_wflat, the
-//     window deal without the ring, drained every round and every tile (8
-//     waves/CU read 3.5 TB/s there).
-// One wave owns its tiles end to end: no workgroup barrier anywhere.
-//
-// Per wave, RF_NB tile buffers in LDS (a tile is planned into buffer s % NB,
-// s = the wave's tile sequence number) hold records by rank {a0 lo, a0 hi,
-// cstart, meta}, the head bitmap per 64-chunk group, the per-descriptor
-// accumulators and edge chunks (as k_flat2) and the phase-4 words; a tile is
-// finished (edge corrections, fold, one 2-B store per descriptor) when the
-// consume side reduces its last group.  The issue side never runs more than
-// NB tiles ahead of the finished ones (it issues placeholder loads instead).
-// Descriptors come two tiles ahead by LDS-DMA (no VGPR is written behind the
-// compiler's back, cf. k_wflat).
-//
-// Wait-count discipline (as k_window's ring, tests/test_isa.py): the group
-// loads, the descriptor DMA are inline asm, one vm operation each, counted in
-// `nvm`; group (k, u) is retired by vmcnt(2U - 1 - u), the U - 1 - u later
-// loads of its round plus the U of the next round being issued after it (the
-// DMAs and result stores in between only make the wait stricter); a plan
-// retires its DMA with vmcnt(vm operations issued since it), exact.
-constexpr uint32_t RF_NB = 4;             // tile buffers per wave
-constexpr uint32_t RF_INV = 0xffffffffu;  // kk of a lane with no chunk
-
-template <int D>
-struct RflatTile {
-    uint4 rec[D];              // by rank: {a0 lo, a0 hi, cstart, meta}
-    uint2 msk[D * FCAP / 64];  // head bitmap per 64-chunk group
-    uint32_t acc[D];           // by descriptor
-    uint4 edge[2 * D];         // by descriptor: raw first / last chunk
-    uint2 fin[D];              // by descriptor: {start_sum, phase-4 word}
-    uint2 info;                // {groups, chunks} of the tile
-};
-
-template <int D>
-struct RflatLds {
-    RflatTile<D> t[SW_WAVES][RF_NB];
-    uint4 pfd[SW_WAVES][2][64];  // descriptors of the next tiles (LDS-DMA)
-};
-
-// s_waitcnt vmcnt(n) for a run-time n (0..23; larger n waits for 23, which
-// is stricter): the plan's wait for its descriptor DMA.
-__device__ __forceinline__ void wait_vm_dyn(uint32_t n) {
-    switch (n < 23u ? n : 23u) {
-#define LVLIP_VMW(K) \
-    case K: asm volatile("s_waitcnt vmcnt(" #K ")" ::: "memory"); break;
-        LVLIP_VMW(0) LVLIP_VMW(1) LVLIP_VMW(2) LVLIP_VMW(3) LVLIP_VMW(4) LVLIP_VMW(5)
-        LVLIP_VMW(6) LVLIP_VMW(7) LVLIP_VMW(8) LVLIP_VMW(9) LVLIP_VMW(10) LVLIP_VMW(11)
-        LVLIP_VMW(12) LVLIP_VMW(13) LVLIP_VMW(14) LVLIP_VMW(15) LVLIP_VMW(16) LVLIP_VMW(17)
-        LVLIP_VMW(18) LVLIP_VMW(19) LVLIP_VMW(20) LVLIP_VMW(21) LVLIP_VMW(22)
-        default: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
-#undef LVLIP_VMW
-    }
-}
-
-__device__ __forceinline__ u32x4 group_load_nt(uint64_t a) {
-    u32x4 r;
-    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(a) : "memory");
-    return r;
-}
-
-template <int N>
-__device__ __forceinline__ void group_wait(u32x4& a) {
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a) : "n"(N) : "memory");
-}
-
-template <int U, int D>
-__global__ __launch_bounds__(256) void k_rflat(const uint8_t* __restrict__ base,
-                                               const lvlip_csum_desc* __restrict__ descs, uint32_t n,
-                                               uint16_t* __restrict__ out) {
-    static_assert(D == 16 || D == 32 || D == 64, "descriptors per tile");
-    static_assert(U >= 2 && 2 * U + 2 <= 23, "group loads per round");
-    __shared__ RflatLds<D> L;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wid = uniform(threadIdx.x >> 6);
-    const uint64_t nw = (uint64_t)gridDim.x * SW_WAVES;
-    const uint64_t rank =
-        (gridDim.x & 7u) == 0u
-            ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * SW_WAVES + wid
-            : (uint64_t)blockIdx.x * SW_WAVES + wid;
-    const uint64_t ntiles = ((uint64_t)n + D - 1) / D;
-    if (rank >= ntiles) return;  // uniform: this wave has no tile
-    // the wave's tiles: rank, rank + nw, ...; count
-    const uint32_t my_tiles = (uint32_t)((ntiles - 1 - rank) / nw + 1);
-    RflatTile<D>* T = L.t[wid];
-    const uint64_t safe = reinterpret_cast<uint64_t>(descs);  // a readable 16-B address
-
-    uint32_t nvm = 0;     // vm operations this wave issued from asm (loads, DMAs)
-    uint32_t pf_at[2];    // nvm when the DMA for the tile of parity p was issued
-
-    // descriptors of the wave's tile s into pfd[s & 1], one per lane (lanes
-    // past the tile or the batch re-read a valid descriptor)
-    auto prefetch = [&](uint32_t s) {
-        const uint64_t t = rank + (uint64_t)s * nw;
-        uint64_t i = t * D + (lane < (uint32_t)D ? lane : 0u);
-        i = i < n ? i : n - 1u;
-        const lvlip_csum_desc* g = descs + i;
-        const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane(
-            (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)L.pfd[wid][s & 1u]);
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-        asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-                     :
-                     : "v"(g), "s"(lds)
-                     : "memory", "m0");
-#pragma clang diagnostic pop
-        pf_at[s & 1u] = nvm;
-        ++nvm;
-    };
-
-    // ---- issue side.  Tiles are planned ahead of the group loads so that a
-    // round's U groups never wait for a plan: s_plan = next tile to plan,
-    // s_iss = the tile whose groups are being issued (cur_g of cur_ng issued),
-    // ahead = planned groups not issued yet.
-    uint32_t s_plan = 0, s_iss = 0;
-    uint32_t cur_b = 0, cur_g = 0, cur_ng = 0, cur_C = 0;
-    uint32_t ahead = 0;
-    uint32_t heads = 0;     // heads in the issue tile's earlier groups
-    uint32_t fin_count = 0; // tiles finished (consume side)
-
-    // plan of tile s into buffer s % NB: records, head bitmaps, accumulators,
-    // phase-4 words, {groups, chunks}; the DMA for tile s + 2 goes out behind it
-    auto plan = [&](uint32_t s) {
-        wait_vm_dyn(nvm - pf_at[s & 1u] - 1u);  // vm ops issued after this tile's DMA
-        const uint4 dv = L.pfd[wid][s & 1u][lane];
-        RflatTile<D>& B = T[s % RF_NB];
-        const uint64_t t = rank + (uint64_t)s * nw;
-        const uint64_t i = t * D + lane;
-        const bool mine = lane < (uint32_t)D && i < n;
-        uint32_t start_sum = 0, nch = 0, meta = 0, fw = 0;
-        uint64_t a0 = 0;
-        if (mine) {
-            const int32_t len = (int32_t)dv.z;
-            start_sum = dv.w;
-            fw = 1u << 21;
-            if (len > 0) {
-                const uint64_t abs = reinterpret_cast<uint64_t>(base) + (((uint64_t)dv.y << 32) | dv.x);
-                a0 = abs & ~15ull;
-                const uint32_t lo = (uint32_t)(abs & 15ull);
-                const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)len;
-                const uint64_t c64 = (span + 15u) >> 4;
-                const uint32_t lastv = (uint32_t)(span - 16ull * (c64 - 1u));  // 1..16
-                const bool big = c64 > FCAP;
-                nch = big ? 0u : (uint32_t)c64;
-                const bool odd = abs & 1ull;
-                const bool ef = !big && (lo != 0u || (c64 == 1u && lastv != 16u));
-                const bool el = !big && c64 > 1u && lastv != 16u;
-                meta = nch | ((uint32_t)odd << 9) | ((uint32_t)ef << 10) | ((uint32_t)el << 11) | (lane << 18);
-                fw |= lo | (lastv << 4) | (nch << 9) | ((uint32_t)odd << 17) | ((uint32_t)ef << 18) |
-                      ((uint32_t)el << 19) | ((uint32_t)big << 20);
-            }
-        }
-        const uint32_t incl = wave_incl_scan(nch);
-        const uint32_t C = uniform((uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
-        const uint32_t cstart = incl - nch;
-        const uint64_t nz = __builtin_amdgcn_ballot_w64(nch != 0u);
-        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
-        const uint32_t ng = C ? (C + 63u) >> 6 : 1u;  // a tile with no chunk still takes one group
-        for (uint32_t q = lane; q < ng; q += 64u) B.msk[q] = make_uint2(0u, 0u);
-        if (lane < (uint32_t)D) {
-            B.acc[lane] = 0u;
-            B.fin[lane] = make_uint2(start_sum, fw);
-        }
-        if (lane == 0u) B.info = make_uint2(ng, C);
-        __builtin_amdgcn_wave_barrier();
-        if (nch) {
-            B.rec[r] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), cstart, meta);
-            const uint32_t q = cstart >> 6, b = cstart & 63u;
-            if (b < 32u) atomicOr(&B.msk[q].x, 1u << b);
-            else atomicOr(&B.msk[q].y, 1u << (b - 32u));
-        }
-        if (s + 2u < my_tiles) prefetch(s + 2u);  // its LDS slot was read above
-        ahead += ng;
-    };
-
-    // finish of the wave's tile fs in buffer fs % NB: the big descriptors, edge
-    // corrections, fold and store (src/utils.c:46-54)
-    auto finish_tile = [&](uint32_t fs) {
-        RflatTile<D>& B = T[fs % RF_NB];
-        lds_sync();  // this tile's accumulator atomics and edge stashes
-        const uint64_t t = rank + (uint64_t)fs * nw;
-        const uint2 f = B.fin[lane < (uint32_t)D ? lane : 0u];
-        const uint32_t fw = lane < (uint32_t)D ? f.y : 0u;
-        uint64_t bigm = __builtin_amdgcn_ballot_w64((fw >> 20) & 1u);
-        if (bigm) {
-            while (bigm) {  // descriptors longer than FCAP chunks: one wave each
-                const uint32_t q = (uint32_t)__builtin_ctzll(bigm);
-                bigm &= bigm - 1ull;
-                const lvlip_csum_desc d = descs[t * D + q];
-                const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
-                const int lo = (int)(abs & 15ull);
-                const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
-                const uint32_t nchq = (uint32_t)((span + 15u) >> 4);
-                const uint32_t lastv = (uint32_t)(span - 16ull * (nchq - 1u));
-                const uint4* src = reinterpret_cast<const uint4*>(abs & ~15ull);
-                uint32_t w = (abs & 1ull) ? wave_packet_sum<4, true>(src, nchq, lo, lastv, lane)
-                                          : wave_packet_sum<4, false>(src, nchq, lo, lastv, lane);
-                w = wave_sum_dpp(w);
-                if (lane == 0) B.acc[q] = w;
-            }
-            lds_sync();
-        }
-        uint32_t acc = B.acc[lane < (uint32_t)D ? lane : 0u];
-        if (fw & (3u << 18)) {
-            const bool odd = fw & (1u << 17);
-            const int lo = (int)(fw & 15u), lastv = (int)((fw >> 4) & 31u);
-            const uint32_t nch = (fw >> 9) & 0xffu;
-            uint32_t c = 0;
-            if (fw & (1u << 18)) {
-                uint4 e = B.edge[2u * lane];
-                const int fb1 = (nch == 1u) ? lastv : 16;
-                e.x &= ~byte_range_mask(lo, fb1, 0);
-                e.y &= ~byte_range_mask(lo, fb1, 1);
-                e.z &= ~byte_range_mask(lo, fb1, 2);
-                e.w &= ~byte_range_mask(lo, fb1, 3);
-                c += odd ? chunk_words<true>(e) : chunk_words<false>(e);
-            }
-            if (fw & (1u << 19)) {
-                uint4 e = B.edge[2u * lane + 1u];
-                e.x &= ~byte_range_mask(0, lastv, 0);
-                e.y &= ~byte_range_mask(0, lastv, 1);
-                e.z &= ~byte_range_mask(0, lastv, 2);
-                e.w &= ~byte_range_mask(0, lastv, 3);
-                c += odd ? chunk_words<true>(e) : chunk_words<false>(e);
-            }
-            acc -= c;
-        }
-        if (fw & (1u << 21)) out[t * D + lane] = finish(f.x, acc);
-        ++fin_count;
-    };
-
-    // Two banks of U group slots; bank X holds one round.  Per slot: the loaded
-    // chunk, the lane's chunk index in its packet (RF_INV: none), the packet's
-    // meta word, and a uniform flag word: 1 valid | 2 last group of its tile |
-    // buffer << 2.
-    u32x4 xa[U], xb[U];
-    uint32_t ka[U], kb[U], ma[U], mb[U], fa[U], fb[U];
-
-    auto issue_round = [&](u32x4* x, uint32_t* kk, uint32_t* mt, uint32_t* fl) {
-        // plan until the round's U groups are planned (or no tile / buffer is left)
-#pragma unroll 1
-        while (ahead < (uint32_t)U && s_plan < my_tiles && s_plan < fin_count + RF_NB) {
-            plan(s_plan);
-            ++s_plan;
-        }
-        uint32_t sb[U], sg[U], sC[U];
-        bool sv[U], sfirst[U], slast[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (cur_g == cur_ng && s_iss < s_plan) {  // the next planned tile
-                cur_b = s_iss % RF_NB;
-                const uint2 info = T[cur_b].info;
-                cur_ng = uniform(info.x);
-                cur_C = uniform(info.y);
-                cur_g = 0;
-                ++s_iss;
-            }
-            sv[u] = cur_g < cur_ng;
-            sb[u] = cur_b;
-            sg[u] = cur_g;
-            sC[u] = cur_C;
-            sfirst[u] = sv[u] && cur_g == 0u;
-            slast[u] = sv[u] && cur_g + 1u == cur_ng;
-            if (sv[u]) {
-                ++cur_g;
-                --ahead;
-            }
-        }
-        uint32_t hlo[U], hhi[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint2 h = T[sb[u]].msk[sv[u] ? sg[u] : 0u];
-            hlo[u] = sv[u] ? uniform(h.x) : 0u;
-            hhi[u] = sv[u] ? uniform(h.y) : 0u;
-        }
-        uint4 rec[U];
-        bool vl[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (sfirst[u]) heads = 0;
-            const uint64_t H = ((uint64_t)hhi[u] << 32) | hlo[u];
-            const uint64_t Hs = H >> 1;
-            const uint32_t cnt = __builtin_amdgcn_mbcnt_hi((uint32_t)(Hs >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)Hs, 0u));
-            const uint32_t rk = heads + (uint32_t)(H & 1ull) + cnt - 1u;
-            heads += (uint32_t)__popcll(H);
-            const uint32_t c = sg[u] * 64u + lane;
-            vl[u] = sv[u] && c < sC[u];
-            rec[u] = T[sb[u]].rec[vl[u] ? rk : 0u];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t c = sg[u] * 64u + lane;
-            kk[u] = vl[u] ? c - rec[u].z : RF_INV;
-            const uint64_t ca = vl[u] ? (((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * (c - rec[u].z) : safe;
-            x[u] = group_load_nt(ca);
-            mt[u] = vl[u] ? rec[u].w : 0u;
-            fl[u] = (uint32_t)sv[u] | ((uint32_t)slast[u] << 1) | (sb[u] << 2);
-        }
-        nvm += U;
-    };
-
-    auto consume_round = [&](u32x4* x, const uint32_t* kk, const uint32_t* mt, const uint32_t* fl) {
-        uint32_t nfin = 0;  // tiles whose last group this round reduced
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            // 2U - 1 - u later group loads were issued: this round's rest and
-            // the next round
-            switch (u) {
-                case 0: group_wait<2 * U - 1>(x[u]); break;
-                case 1: group_wait<2 * U - 2>(x[u]); break;
-                case 2: group_wait<2 * U - 3>(x[u]); break;
-                case 3: group_wait<2 * U - 4>(x[u]); break;
-                case 4: group_wait<2 * U - 5>(x[u]); break;
-                case 5: group_wait<2 * U - 6>(x[u]); break;
-                case 6: group_wait<2 * U - 7>(x[u]); break;
-                default: group_wait<2 * U - 8>(x[u]); break;
-            }
-            const uint32_t f = uniform(fl[u]);
-            if (!(f & 1u)) continue;  // uniform: a placeholder
-            RflatTile<D>& B = T[f >> 2];
-            const u32x4 raw = x[u];
-            uint4 v = make_uint4(raw.x, raw.y, raw.z, raw.w);
-            const uint32_t m = mt[u];
-            const bool vlu = kk[u] != RF_INV;
-            if (__builtin_amdgcn_ballot_w64((m & (1u << 9)) != 0u)) {
-                const uint32_t sel = (m & (1u << 9)) ? 0x02030001u : 0x03020100u;
-                v.x = __builtin_amdgcn_perm(v.x, v.x, sel);
-                v.y = __builtin_amdgcn_perm(v.y, v.y, sel);
-                v.z = __builtin_amdgcn_perm(v.z, v.z, sel);
-                v.w = __builtin_amdgcn_perm(v.w, v.w, sel);
-            }
-            uint32_t val = 0;
-            val = dot2_acc(v.x, val);
-            val = dot2_acc(v.y, val);
-            val = dot2_acc(v.z, val);
-            val = dot2_acc(v.w, val);
-            val = vlu ? val : 0u;
-            const uint32_t P = wave_incl_scan(val);
-            const bool first = kk[u] == 0u;
-            const bool last = vlu && kk[u] + 1u == (m & 0xFFu);
-            const uint32_t add = (first ? val - P : 0u) + ((last || lane == 63u) ? P : 0u);
-            const uint32_t slot = (m >> 18) & 63u;
-            if (vlu && (first || last || lane == 63u)) atomicAdd(&B.acc[slot], add);
-            if (vlu && first && (m & (1u << 10))) B.edge[2u * slot] = make_uint4(raw.x, raw.y, raw.z, raw.w);
-            if (vlu && last && (m & (1u << 11))) B.edge[2u * slot + 1u] = make_uint4(raw.x, raw.y, raw.z, raw.w);
-            nfin += (f >> 1) & 1u;
-        }
-#pragma unroll 1
-        for (; nfin; --nfin) finish_tile(fin_count);
-    };
-
-    prefetch(0);
-    if (my_tiles > 1u) prefetch(1);
-    issue_round(xa, ka, ma, fa);
-    for (;;) {
-        issue_round(xb, kb, mb, fb);
-        consume_round(xa, ka, ma, fa);
-        if (fin_count == my_tiles) break;
-        issue_round(xa, ka, ma, fa);
-        consume_round(xb, kb, mb, fb);
-        if (fin_count == my_tiles) break;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this wave left in flight
-}
-
 // ------------------------------------------ k_echo_reply (f4, RFC 1624) --
 //
 // icmpv4_reply (src/icmpv4.c:31-54) turns an echo request into the reply by
@@ -759,33 +380,6 @@ bool launch_lane(int lanes, int per_group, int chunks, int mode, hipStream_t s, 
     }
 }
 
-// k_rflat: waves_per_cu waves on every CU (fewer when the batch has fewer
-// tiles); the grid stays a multiple of 8 blocks when it can (XCD-major ranks).
-template <int U, int D>
-void launch_rflat_ud(int waves_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d,
-                     uint32_t n, uint16_t* out) {
-    uint64_t waves = (uint64_t)current_cus() * (uint64_t)waves_per_cu;
-    const uint64_t nt = ((uint64_t)n + D - 1) / D;
-    if (waves > nt) waves = nt;
-    uint64_t grid = (waves + lvlip::SW_WAVES - 1) / lvlip::SW_WAVES;
-    if (grid > 8) grid = grid & ~7ull;
-    hipLaunchKernelGGL((lvlip::k_rflat<U, D>), dim3((uint32_t)grid), dim3(256), 0, s,
-                       (const uint8_t*)base, d, n, out);
-}
-
-bool launch_rflat(int u, int tile, int waves_per_cu, hipStream_t s, const void* base,
-                  const lvlip_csum_desc* d, uint32_t n, uint16_t* out) {
-    switch (u * 1000 + tile) {
-#define LVLIP_RF(UU, DD) \
-    case UU * 1000 + DD: launch_rflat_ud<UU, DD>(waves_per_cu, s, base, d, n, out); return true;
-        LVLIP_RF(2, 16) LVLIP_RF(4, 16) LVLIP_RF(6, 16) LVLIP_RF(8, 16)
-        LVLIP_RF(2, 32) LVLIP_RF(4, 32) LVLIP_RF(6, 32) LVLIP_RF(8, 32)
-        LVLIP_RF(4, 64) LVLIP_RF(8, 64)
-#undef LVLIP_RF
-        default: return false;
-    }
-}
-
 // AUTO's k_lane range: hints below this many bytes (scripts/shape_sweep.py,
 // DESIGN.md §4).
 constexpr int kLaneHintMax = 33;
@@ -858,17 +452,6 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
                 case 4: launch_window<4>(w, s, base, descs, n, out, group, hint); break;
                 default: return LVLIP_EINVAL;
             }
-            break;
-        }
-        case LVLIP_KERNEL_RFLAT: {
-            // unroll = 64-chunk group loads per round (low byte: 2, 4, 6, 8;
-            // 0 = 4) | descriptors per tile << 8 (16, 32, 64; 0 = 16); 12
-            // waves/CU by default
-            if (unroll < 0 || (unroll >> 16) != 0) return LVLIP_EINVAL;
-            int u = unroll & 0xff, tile = (unroll >> 8) & 0xff;
-            if (u == 0) u = 4;
-            if (tile == 0) tile = 16;
-            if (!launch_rflat(u, tile, wpc > 0 ? wpc : 12, s, base, descs, n, out)) return LVLIP_EINVAL;
             break;
         }
         case LVLIP_KERNEL_LANE: {

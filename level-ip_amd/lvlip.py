@@ -29,12 +29,13 @@ LAB_PATH = os.path.join(HERE, "liblvlip_lab.so")
 # error codes (include/lvlip_csum.h)
 OK, EINVAL, ENODEV, EHIP, ENOMEM, ERANGE = 0, -1, -2, -3, -4, -5
 # the product's kernels (include/lvlip_csum.h)
-KERNEL_AUTO, KERNEL_FLAT, KERNEL_WINDOW, KERNEL_LANE, KERNEL_RFLAT = 0, 3, 8, 10, 11
+KERNEL_AUTO, KERNEL_FLAT, KERNEL_WINDOW, KERNEL_LANE = 0, 3, 8, 10
 # the A/B variants measured against them, in liblvlip_lab.so (lab_kernels.hip);
 # batch_dev sends these ids (and FLAT's A/B shapes) there, the product
 # returns EINVAL for them.  6 and 7 are retired round-1 ids (EINVAL everywhere).
 KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_WAVE_SIMPLE, KERNEL_FLAT_V1, KERNEL_WFLAT = 1, 2, 4, 5, 9
-LAB_KERNELS = (KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_WAVE_SIMPLE, KERNEL_FLAT_V1, KERNEL_WFLAT)
+KERNEL_RFLAT = 11
+LAB_KERNELS = (KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_WAVE_SIMPLE, KERNEL_FLAT_V1, KERNEL_WFLAT, KERNEL_RFLAT)
 REG_DMA, REG_ZEROCOPY = 0, 1
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "wave_lds": KERNEL_WAVE_LDS,
                 "flat": KERNEL_FLAT, "wave_simple": KERNEL_WAVE_SIMPLE, "flat_v1": KERNEL_FLAT_V1,

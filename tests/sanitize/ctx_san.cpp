@@ -140,6 +140,7 @@ static void frame_calls(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed) {
 }
 
 int main() {
+    printf("build_id: %s\n", lvlip_build_id());
     if (lvlip_device_count() < 1) {
         fprintf(stderr, "no HIP device\n");
         return 2;

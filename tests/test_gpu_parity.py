@@ -462,7 +462,7 @@ def test_retired_and_lab_ids_rejected_by_the_product():
     L = lvlip.lib()
     for k, u in ((6, 0), (7, 0), (lvlip.KERNEL_WAVE, 2), (lvlip.KERNEL_WAVE_LDS, 2),
                  (lvlip.KERNEL_WAVE_SIMPLE, 2), (lvlip.KERNEL_FLAT_V1, 0), (lvlip.KERNEL_WFLAT, 0),
-                 (lvlip.KERNEL_FLAT, 6), (lvlip.KERNEL_FLAT, 4 | (2 << 8))):
+                 (lvlip.KERNEL_FLAT, 6), (lvlip.KERNEL_FLAT, 4 | (2 << 8)), (lvlip.KERNEL_RFLAT, 0)):
         cfg = lvlip.LaunchCfg(k, u, 0, 0)
         assert L.lvlip_csum_batch_dev_ex(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None,
                                          ctypes.byref(cfg)) == lvlip.EINVAL, (k, u)

@@ -28,3 +28,7 @@ def test_host_batches_under_asan():
     assert r.returncode == 0, out[-4000:]
     assert "ERROR: AddressSanitizer" not in out, out[-4000:]
     assert "all checks passed" in r.stdout
+    # built from this tree's product sources (the same hash as the library's)
+    import lvlip
+
+    assert f"build_id: {lvlip.source_build_id()}" in r.stdout, r.stdout[:200]
