@@ -49,10 +49,11 @@ def check_line(line: dict, steps: int, warmup: int):
 
 
 # committed line -> (algorithmic bytes per launch, bound on PMC traffic / algorithmic)
+TAG = "r03"
 COMMITTED = {
-    "r02_bench_tcp1500.json": (TCP1500_BYTES, 1.05),
-    "r02_bench_tcp9000.json": (1_048_576 * 9000, 1.05),
-    "r02_bench_mixed.json": (1_639_948_630, 1.15),  # layout + descriptors, DESIGN.md §5
+    f"{TAG}_bench_tcp1500.json": (TCP1500_BYTES, 1.05),
+    f"{TAG}_bench_tcp9000.json": (1_048_576 * 9000, 1.05),
+    f"{TAG}_bench_mixed.json": (1_639_948_630, 1.15),  # layout + descriptors, DESIGN.md §5
 }
 # the device function AUTO runs for each committed line (bench.py KERNEL_FN)
 DOMINANT = {"tcp1500": "k_window", "tcp9000": "k_window", "mixed": "k_flat2"}
@@ -82,8 +83,8 @@ def test_committed_bench_line_consistent(name):
     assert line["roofline"]["algo_bytes_per_launch"] == algo
     # the PMC traffic is per launch and within a few % of the algorithmic bytes
     # (committed beside the line; the line itself carries it once that file exists)
-    wl = name[len("r02_bench_"):-len(".json")]
-    with open(os.path.join(PROF, f"r02_pmc_{wl}.json")) as f:
+    wl = name[len(f"{TAG}_bench_"):-len(".json")]
+    with open(os.path.join(PROF, f"{TAG}_pmc_{wl}.json")) as f:
         pmc = json.load(f)["kernels"][0]
     assert pmc["kernel_regex"] == DOMINANT[wl] and pmc["algo_bytes_per_launch"] == algo
     assert 1.0 <= pmc["hbm_bytes_per_launch"] / algo < max_ratio
@@ -93,18 +94,27 @@ def test_committed_bench_line_consistent(name):
     cb = line["cpu_baseline"]
     assert cb["kind"] in ("reference", "port") and cb["cores"] >= 1
     assert cb["unit"] == "GB/s" and cb["value"] > 0 and cb["sample"]
+    # the host's CPU count and model are stated, and the threads
+    # used are the CPUs the process may use (affinity mask under the cgroup quota)
+    assert cb["nproc"] >= cb["cores_used"] == cb["cores"] and cb["cpu_model"]
+    if cb["cgroup_cpu_quota"]:
+        assert cb["cores"] <= cb["cgroup_cpu_quota"] + 1
+    # the whole timed batch was checked against the reference, on every rank
+    assert line["diag"]["verify"]["descriptors"] == line["config"]["descriptors_per_gpu"]
+    assert line["diag"]["verify"]["mismatches"] == 0
+    assert line["dist"]["world_size"] == 1 and line["roofline"]["frac_aggregate"] > 0
 
 
 @pytest.mark.parametrize("wl", sorted(DOMINANT))
 def test_committed_trace_matches_bench_line(wl):
-    with open(os.path.join(PROF, f"r02_bench_{wl}.json")) as f:
+    with open(os.path.join(PROF, f"{TAG}_bench_{wl}.json")) as f:
         line = json.loads(f.read().strip().splitlines()[-1])
-    with open(os.path.join(PROF, f"r02_{wl}_kernel_stats.csv")) as f:
+    with open(os.path.join(PROF, f"{TAG}_{wl}_kernel_stats.csv")) as f:
         rows = {r["Name"]: r for r in csv.DictReader(f)}
     ks = rows[DOMINANT[wl]]
     # the clock-settle launches (~1 000, their count varies with the run) + 50
-    # warm-ups + 200 timed launches + 1 verification launch of the same command
-    assert int(ks["Calls"]) >= 251 + 8
+    # warm-ups + 200 timed launches of the same command
+    assert int(ks["Calls"]) >= 250 + 8
     avg_ms = float(ks["AverageNs"]) * 1e-6
     assert avg_ms == pytest.approx(line["roofline"]["kernel_ms"], rel=0.03)
 
