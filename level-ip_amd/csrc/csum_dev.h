@@ -28,6 +28,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "flat_src.h"
 #include "lvlip_csum.h"
@@ -545,6 +546,20 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+// A ring's 16-B group load, `global_load_dwordx4 ... nt` from asm (k_flat2's
+// pipelined sweep, lab k_rflat): the compiler's wait-count pass does not see
+// it, so the ring's own counted waits retire it.
+__device__ __forceinline__ u32x4 group_load_nt(uint64_t a) {
+    u32x4 r;
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(a) : "memory");
+    return r;
+}
+
+template <int N>
+__device__ __forceinline__ void group_wait(u32x4& a) {
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a) : "n"(N) : "memory");
+}
+
 // two exclusive prefixes over the 256 threads for one barrier pair; *ta, *tb
 // get the totals
 __device__ __forceinline__ void block_excl_scan2(uint32_t a, uint32_t b, uint32_t* s_tmp /* >= 8 */,
@@ -596,10 +611,11 @@ __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
 // plan's share of the launch (A/B, batch calls only; unroll bit 10).  Thread t
 // owns the tile's descriptors t*D .. t*D + D - 1, so its ranks, chunk starts
 // and big-packet slots follow from one exclusive scan of its D counts.
-template <int U, bool NT, int GORD, class Src, int D = 1>
+template <int U, bool NT, int GORD, class Src, int D = 1, bool PIPE = false>
 __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, const Src src,
                                               uint32_t n) {
     static_assert(D == 1 || D == 2, "descriptors per thread");
+    static_assert(!PIPE || (NT && U <= 8), "the pipelined sweep: nontemporal, at most 8 loads per round");
     constexpr uint32_t TD = (uint32_t)FT * D;   // descriptors per tile
     constexpr uint32_t FG = TD * FCAP / 64;     // most 64-chunk groups a tile can have
     __shared__ uint4 s_rec[TD];        // by rank: {a0 lo, a0 hi, cstart, meta}
@@ -746,7 +762,106 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
     const uint32_t gper = (G + 3u) / 4u;
     const uint32_t g_lo = GORD == 1 ? wid * gper : (GORD == 2 ? wid * (uint32_t)U : wid);
     const uint32_t g_end = GORD == 1 ? (g_lo + gper < G ? g_lo + gper : G) : G;
-    if (C > 0) {
+    if (PIPE && C > 0) {
+        // Pipelined sweep (A/B, lab): two rounds' loads (two register banks)
+        // are issued before the first is reduced, so the second round's loads
+        // are in flight during the first's reduction instead of being issued
+        // after it.  The loads are asm (group_load_nt) and retired by counted
+        // waits: a load of the first bank has its bank's later loads and the
+        // second bank's U behind it, a load of the second only its own bank's
+        // (a round past the wave's groups is a placeholder round of valid
+        // loads, so the counts hold).
+        u32x4 xa[U], xb[U];
+        uint32_t mta[U], mtb[U], kka[U], kkb[U];
+        bool vla[U], vlb[U], gva[U], gvb[U];
+        auto prep = [&](uint32_t gr, u32x4* x, uint32_t* mt, uint32_t* kk, bool* vl, bool* gv) {
+            uint32_t hlo[U], hhi[U], hb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t g = gr + gstep * u;
+                gv[u] = g < g_end;
+                const uint32_t gc = gv[u] ? g : G - 1u;
+                const uint2 gg = s_grp[gc];
+                hlo[u] = uniform(gg.x);
+                hhi[u] = uniform(gg.y);
+                hb[u] = uniform((uint32_t)s_hb[gc]);
+            }
+            uint4 rec[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t H = ((uint64_t)hhi[u] << 32) | hlo[u];
+                const uint64_t Hs = H >> 1;
+                const uint32_t cnt = __builtin_amdgcn_mbcnt_hi((uint32_t)(Hs >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)Hs, 0u));
+                rec[u] = s_rec[(hb[u] + (uint32_t)(H & 1ull) - 1u) + cnt];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t j = (gr + gstep * u) * 64u + lane;
+                vl[u] = gv[u] && j < C;
+                kk[u] = vl[u] ? j - rec[u].z : 0u;
+                x[u] = group_load_nt((((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * kk[u]);
+                mt[u] = rec[u].w;
+            }
+        };
+        auto reduce = [&](auto depth, u32x4* x, const uint32_t* mt, const uint32_t* kk, const bool* vl,
+                          const bool* gv) {
+            constexpr int B = decltype(depth)::value;  // loads issued after a bank's first
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                switch (u) {
+                    case 0: group_wait<(B > 1 ? B - 1 : 0)>(x[u]); break;
+                    case 1: group_wait<(B > 2 ? B - 2 : 0)>(x[u]); break;
+                    case 2: group_wait<(B > 3 ? B - 3 : 0)>(x[u]); break;
+                    case 3: group_wait<(B > 4 ? B - 4 : 0)>(x[u]); break;
+                    case 4: group_wait<(B > 5 ? B - 5 : 0)>(x[u]); break;
+                    case 5: group_wait<(B > 6 ? B - 6 : 0)>(x[u]); break;
+                    case 6: group_wait<(B > 7 ? B - 7 : 0)>(x[u]); break;
+                    default: group_wait<(B > 8 ? B - 8 : 0)>(x[u]); break;
+                }
+                if (!gv[u]) continue;  // uniform: past the wave's groups (waited all the same)
+                const u32x4 raw = x[u];
+                uint4 v = make_uint4(raw.x, raw.y, raw.z, raw.w);
+                const uint32_t m = mt[u];
+                if (__builtin_amdgcn_ballot_w64((m & (1u << 9)) != 0u)) {
+                    const uint32_t sel = (m & (1u << 9)) ? 0x02030001u : 0x03020100u;
+                    v.x = __builtin_amdgcn_perm(v.x, v.x, sel);
+                    v.y = __builtin_amdgcn_perm(v.y, v.y, sel);
+                    v.z = __builtin_amdgcn_perm(v.z, v.z, sel);
+                    v.w = __builtin_amdgcn_perm(v.w, v.w, sel);
+                }
+                uint32_t val = 0;
+                val = dot2_acc(v.x, val);
+                val = dot2_acc(v.y, val);
+                val = dot2_acc(v.z, val);
+                val = dot2_acc(v.w, val);
+                val = vl[u] ? val : 0u;
+                const uint32_t P = wave_incl_scan(val);
+                const bool first = kk[u] == 0u;
+                const bool last = kk[u] + 1u == (m & 0xFFu);
+                const uint32_t add = (first ? val - P : 0u) + ((last || lane == 63u) ? P : 0u);
+                if (vl[u] && (first || last || lane == 63u)) atomicAdd(&s_acc[m >> 18], add);
+                if (vl[u] && first && (m & (1u << 10)))
+                    s_edge[2u * (m >> 18)] = make_uint4(raw.x, raw.y, raw.z, raw.w);
+                if (vl[u] && last && (m & (1u << 11)))
+                    s_edge[2u * (m >> 18) + 1u] = make_uint4(raw.x, raw.y, raw.z, raw.w);
+            }
+        };
+        // Rounds in pairs: the second round's loads are in flight while the
+        // first is reduced, and nothing is in flight across the loop's back
+        // edge.  (A version that carried a bank in flight across the back edge
+        // let the register allocator copy a bank's registers at the loop head
+        // before their loads had landed: wrong sums, caught by the parity tests
+        // and by tests/test_isa.py's in-flight register check.)
+        using Two = std::integral_constant<int, 2 * U>;
+        using One = std::integral_constant<int, U>;
+        for (uint32_t gr = g_lo; gr < g_end; gr += 2u * rstep) {
+            prep(gr, xa, mta, kka, vla, gva);
+            prep(gr + rstep, xb, mtb, kkb, vlb, gvb);  // placeholders past g_end
+            reduce(Two{}, xa, mta, kka, vla, gva);
+            reduce(One{}, xb, mtb, kkb, vlb, gvb);
+        }
+    } else if (C > 0) {
         for (uint32_t gr = g_lo; gr < g_end; gr += rstep) {
             uint4 x[U];
             uint32_t mt[U], kk[U];

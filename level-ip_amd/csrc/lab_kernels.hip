@@ -578,17 +578,6 @@ __device__ __forceinline__ void wait_vm_dyn(uint32_t n) {
     }
 }
 
-__device__ __forceinline__ u32x4 group_load_nt(uint64_t a) {
-    u32x4 r;
-    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(a) : "memory");
-    return r;
-}
-
-template <int N>
-__device__ __forceinline__ void group_wait(u32x4& a) {
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a) : "n"(N) : "memory");
-}
-
 template <int U, int D>
 __global__ __launch_bounds__(256) void k_rflat(const uint8_t* __restrict__ base,
                                                const lvlip_csum_desc* __restrict__ descs, uint32_t n,
@@ -1101,10 +1090,25 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             // k_flat2's A/B shapes: loads per round | group order + 1 << 8 (1
             // interleaved, 2 quarters, 3 blocks; 0 = LVLIP_FLAT_GROUPS, else
             // blocks) | 1 << 10 for tiles of 512 descriptors (U 4 or 8,
-            // quarters or blocks); LVLIP_LOAD_POLICY=temporal for plain loads
+            // quarters or blocks) | 1 << 11 for the pipelined sweep (U 2, 4,
+            // 6, 8; blocks); LVLIP_LOAD_POLICY=temporal for plain loads
             const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
             if (unroll < 0) unroll = 0;
-            if ((unroll >> 11) != 0) return LVLIP_EINVAL;
+            if ((unroll >> 12) != 0) return LVLIP_EINVAL;
+            if ((unroll >> 11) & 1) {
+                if ((unroll >> 8) & 7) return LVLIP_EINVAL;
+                switch (unroll & 0xff) {
+#define LVLIP_FLAT_PIPE(UU)                                                                        \
+    case UU:                                                                                       \
+        hipLaunchKernelGGL((lvlip::k_flat2<UU, true, 2, lvlip::DescSrc, 1, true>), dim3(grid),     \
+                           dim3(lvlip::FT), 0, s, (const uint8_t*)base, lvlip::DescSrc{descs, out}, n); \
+        break;
+                    LVLIP_FLAT_PIPE(2) LVLIP_FLAT_PIPE(4) LVLIP_FLAT_PIPE(6) LVLIP_FLAT_PIPE(8)
+#undef LVLIP_FLAT_PIPE
+                    default: return LVLIP_EINVAL;
+                }
+                break;
+            }
             const int uo = (unroll >> 8) & 3;
             const bool d2 = (unroll >> 10) & 1;
             unroll &= 0xFF;

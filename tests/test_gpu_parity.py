@@ -45,6 +45,10 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT, 2 | (3 << 8), 0),
     (lvlip.KERNEL_FLAT, 8 | (1 << 10), 0),            # tiles of 512: 2 descriptors per thread
     (lvlip.KERNEL_FLAT, 4 | (2 << 8) | (1 << 10), 0),
+    (lvlip.KERNEL_FLAT, 2 | (1 << 11), 0),            # pipelined sweep (lab A/B)
+    (lvlip.KERNEL_FLAT, 4 | (1 << 11), 0),
+    (lvlip.KERNEL_FLAT, 6 | (1 << 11), 0),
+    (lvlip.KERNEL_FLAT, 8 | (1 << 11), 0),
     (5, 0, 0),                     # first-generation flat kernel (A/B)
     (lvlip.KERNEL_WINDOW, 3, 0),   # interleaved stream: groups dealt round robin
     (lvlip.KERNEL_WINDOW, 2, 1),   # 1 wave/CU: long per-wave sequences, window refills
@@ -233,6 +237,7 @@ def test_full_size_bit_exact(name):
                     (lvlip.KERNEL_WINDOW, 3, 0), (lvlip.KERNEL_WINDOW, 2, 0),
                     (lvlip.KERNEL_WFLAT, 0, 0), (lvlip.KERNEL_WFLAT, 8 | (64 << 8), 16),
                     (lvlip.KERNEL_RFLAT, 0, 0), (lvlip.KERNEL_RFLAT, 8 | (32 << 8), 8),
+                    (lvlip.KERNEL_FLAT, 4 | (1 << 11), 0), (lvlip.KERNEL_FLAT, 8 | (1 << 11), 0),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
                     (lvlip.KERNEL_FLAT, 8 | (1 << 10), 0),
@@ -439,7 +444,8 @@ def test_bad_launch_shapes_rejected():
     out = torch.empty(1, dtype=torch.int16, device="cuda")
     for k, u in ((lvlip.KERNEL_FLAT, 3), (lvlip.KERNEL_FLAT, 6 | (1 << 10)),
                  (lvlip.KERNEL_FLAT, 8 | (1 << 8) | (1 << 10)), (lvlip.KERNEL_FLAT, 2 | (1 << 10)),
-                 (lvlip.KERNEL_FLAT, 8 | (1 << 11)),
+                 (lvlip.KERNEL_FLAT, 8 | (1 << 12)), (lvlip.KERNEL_FLAT, 3 | (1 << 11)),
+                 (lvlip.KERNEL_FLAT, 4 | (1 << 8) | (1 << 11)),
                  (lvlip.KERNEL_WINDOW, 2 | (5 << 8)), (lvlip.KERNEL_WFLAT, 8 | (48 << 8)),
                  (lvlip.KERNEL_LANE, 3), (lvlip.KERNEL_LANE, 4 | (5 << 8)),
                  (lvlip.KERNEL_LANE, 4 | (1 << 8) | (3 << 16)),

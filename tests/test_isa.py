@@ -117,6 +117,41 @@ def test_ring_waits_are_counted_not_draining(asm):
         assert len(drains) <= 2, (name, waits)
 
 
+def test_pipelined_flat_sweep_registers_not_read_in_flight(asm):
+    """The lab's pipelined k_flat2 sweep (FLAT unroll bit 11): no path from a
+    ring load to its retiring wait touches the load's destination registers
+    (the bank-across-the-back-edge version failed this and the parity tests)."""
+    from isa_inflight import inflight_hazards
+
+    f = functions_with_labels(asm)
+    ks = {n: b for n, b in f.items() if "k_flat2" in n and "DescSrcELi1ELb1E" in n}
+    assert len(ks) == 4, sorted(ks)
+    for name, body in ks.items():
+        h = inflight_hazards(body, r"global_load_dwordx4 v\[\d+:\d+\], v\[\d+:\d+\], off nt")
+        assert not h, (name, h[:3])
+
+
+def functions_with_labels(text):
+    """name -> instruction lines with block labels kept (for the flow check)."""
+    funcs, cur = {}, None
+    for line in text.splitlines():
+        m = re.match(r"^(_Z\w+):", line)
+        if m:
+            cur = []
+            funcs[m.group(1)] = cur
+            continue
+        if cur is None:
+            continue
+        if line.startswith(".Lfunc_end"):
+            cur = None
+            continue
+        s = line.split(";")[0].strip()
+        if not s or (s.startswith(".") and not s.endswith(":")):
+            continue
+        cur.append(s)
+    return funcs
+
+
 def test_no_scratch(asm):
     for m in re.finditer(r"\.name:\s+(_Z\w*k_(?:stream|window)\w*)\n(?:.*\n){0,60}?\s+\.private_segment_fixed_size:\s+(\d+)",
                          asm):
