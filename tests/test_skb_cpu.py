@@ -333,7 +333,7 @@ def test_icmp_incremental_refuses_non_requests():
 
 def test_frame_calls_refuse_oversized_batches():
     """A frame yields up to two checksums, so the host frame calls take at most
-    LVLIP_MAX_BATCH / 2 frames, like the _dev calls (skb_dev.hip): larger n is
+    LVLIP_MAX_BATCH / 2 frames, like the _dev calls (csum_kernels.hip): larger n is
     LVLIP_EINVAL before the context, the frames or any allocation are touched
     (the dummy pointers below are never dereferenced)."""
     L = lvlip.lib()
