@@ -519,6 +519,10 @@ int launch_rx_hdr(const void* base, const lvlip_frame_desc* frames, uint32_t n, 
 
 constexpr uint32_t kMaxFrames = LVLIP_MAX_BATCH / 2u;  // two entries per frame
 
+// k_window batches of many groups per wave run as launches of about this many
+// groups per wave (lvlip_csum_batch_dev_ex)
+constexpr uint64_t kWindowGroupsPerWave = 80;
+
 }  // namespace
 
 extern "C" {
@@ -562,9 +566,32 @@ int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint
     if (n == 0) return LVLIP_OK;
     if (!base || !descs || !out || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
     if (((uintptr_t)base & 15u) != 0) return LVLIP_EINVAL;
+    // AUTO resolved once for the whole batch (its shape depends on n)
+    lvlip_launch_cfg c = cfg ? *cfg : lvlip_launch_cfg{LVLIP_KERNEL_AUTO, 0, 0, 0};
+    if (c.kernel == LVLIP_KERNEL_AUTO) c.kernel = auto_select(c.len_hint, n, &c.unroll, &c.waves_per_cu);
+    // Long k_window launches lose rate: the persistent waves drift apart over
+    // a launch, and the window of the batch they read widens.  A batch of more
+    // than 1.5 x kWindowGroupsPerWave groups per wave goes out as launches of
+    // about kWindowGroupsPerWave groups per wave, back to back on the stream,
+    // which restart the waves in step (scripts/split_tune_once.sh:
+    // 8M MTU segments 6 725 GB/s in one launch, 6 866 in 8; 64M 6 450 in one,
+    // 6 850 in 64; 1M jumbo 7 113 in one, 7 146 in 2).  The configs' 1M MTU
+    // batch (85 groups per wave) stays one launch.  Results are the same bits:
+    // each launch checksums its own descriptor range.
+    uint32_t piece = kLaunchMax;
+    if (c.kernel == LVLIP_KERNEL_WINDOW) {
+        const int g = window_group((c.unroll >> 8) & 0xff, c.len_hint);
+        const uint64_t waves = (uint64_t)current_cus() * (uint64_t)(c.waves_per_cu > 0 ? c.waves_per_cu : 8);
+        const uint64_t per_launch = waves * (uint64_t)g * kWindowGroupsPerWave;
+        if ((uint64_t)n > per_launch + per_launch / 2u) {
+            const uint64_t parts = ((uint64_t)n + per_launch / 2u) / per_launch;
+            const uint64_t per = ((uint64_t)n + parts - 1) / parts;
+            if (per < piece) piece = (uint32_t)per;
+        }
+    }
     for (uint32_t lo = 0; lo < n;) {
-        const uint32_t m = n - lo < kLaunchMax ? n - lo : kLaunchMax;
-        const int rc = dispatch_one(base, descs + lo, m, out + lo, (hipStream_t)stream, cfg);
+        const uint32_t m = n - lo < piece ? n - lo : piece;
+        const int rc = dispatch_one(base, descs + lo, m, out + lo, (hipStream_t)stream, &c);
         if (rc != LVLIP_OK) return rc;
         lo += m;
     }

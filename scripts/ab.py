@@ -43,7 +43,7 @@ def main():
     wl = os.environ.get("AB_WORKLOAD", "tcp1500")
     rounds = int(os.environ.get("AB_ROUNDS", "5"))
     dev = torch.device("cuda", 0)
-    b = workloads.make(wl)
+    b = workloads.make(wl, n=int(os.environ["AB_N"]) if os.environ.get("AB_N") else None)
     base, descs, out = workloads.to_device(b, dev)
     s = torch.cuda.current_stream(dev)
     hint = b.algo_bytes // b.n
@@ -79,7 +79,7 @@ def main():
             return f
         return lambda: lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
                                        s.cuda_stream, lvlip.KERNEL_NAMES[k], u, w, h)
-    timed(mk("auto", 0, 0, hint), s, reps=400)  # clock settle
+    timed(mk("auto", 0, 0, hint), s, reps=int(os.environ.get("AB_SETTLE", "400")))  # clock settle
     ref, res = None, {}
     for rnd in range(rounds):
         for key, k, u, w, h in variants:
