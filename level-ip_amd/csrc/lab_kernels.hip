@@ -10,6 +10,8 @@
 //   k_wflat        k_flat2's sweep one wave per tile, tiles dealt round robin (9)
 //   k_rflat        the same with a ring of group loads across tiles (11;
 //                  round 3, DESIGN.md §4: instruction-bound, 4.0 vs 6.2 TB/s)
+//   k_wsflat       k_flat2's sweep in persistent workgroups of 4 sweeper
+//                  waves + 1 planner wave, tiles double-buffered (12)
 //   k_flat2        its other shapes (3): group orders, tiles of 512, temporal
 //                  loads, U 6 / 12, an LDS pad; and the frame calls' variants
 //                  (8 loads per round, block order, plain field stores, the
@@ -879,6 +881,268 @@ __global__ __launch_bounds__(256) void k_rflat(const uint8_t* __restrict__ base,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this wave left in flight
 }
 
+
+// ------------------------------------ k_wsflat (warp-specialized, lab 12) --
+//
+// k_flat2's tile with its planning taken off the sweep's critical path.  A
+// workgroup is WS_SW sweeper waves and one planner wave, persistent (a few per
+// CU), its tiles dealt round robin over the workgroups (XCD-major ranks) so the
+// resident workgroups read one window of the batch.  Two tile buffers in LDS:
+// while the sweepers sweep tile k (buffer k & 1, k_flat2's phase 2 unchanged),
+// the planner finishes tile k - 1 (phase 3 + 4: big packets, edge corrections,
+// fold, stores) and plans tile k + 1 (phase 1, one wave-level scan per 64
+// descriptors) into the other buffer; one workgroup barrier per tile hands the
+// buffers over.  The descriptors of tile k + 1 are loaded at the start of the
+// planner's iteration, so their latency hides behind the finish of tile k - 1.
+// The sweepers see no phase-1/phase-4 bubbles and no per-tile launch; the
+// question this kernel answers is whether k_flat2's gap on
+// mixed is those bubbles or its access order.
+constexpr int WS_SW = 4;  // sweeper waves per workgroup
+
+template <int TD>
+struct WsBuf {
+    static constexpr uint32_t FG = (uint32_t)TD * FCAP / 64;
+    uint4 rec[TD];       // by rank: {a0 lo, a0 hi, cstart, meta} (k_flat2's meta)
+    uint4 edge[2 * TD];  // by descriptor: raw first / last chunk
+    uint2 grp[FG];       // by 64-chunk group: head bitmap
+    uint2 fin[TD];       // by descriptor: {start_sum, nch | odd 9 | ef 10 | el 11 | lo << 12 | lastv << 16}
+    uint32_t acc[TD];    // by descriptor
+    uint32_t big[TD];    // descriptors longer than FCAP chunks
+    uint16_t hb[FG];     // by 64-chunk group: heads before it
+    uint32_t C, nbig;
+};
+
+template <int U, int TD, int GORD>
+__global__ __launch_bounds__((WS_SW + 1) * 64) void k_wsflat(const uint8_t* __restrict__ base,
+                                                             const lvlip_csum_desc* __restrict__ descs,
+                                                             uint32_t n, uint16_t* __restrict__ out) {
+    static_assert(TD == 64 || TD == 128 || TD == 256, "descriptors per tile");
+    constexpr uint32_t NP = TD / 64;  // planner passes per tile
+    constexpr uint32_t FG = WsBuf<TD>::FG;
+    __shared__ WsBuf<TD> B[2];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = uniform(threadIdx.x >> 6);
+    const bool planner = wid == (uint32_t)WS_SW;
+    const uint32_t nwg = gridDim.x;
+    const uint32_t rank = (nwg & 7u) == 0u ? (blockIdx.x & 7u) * (nwg >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const uint32_t ntiles = (uint32_t)(((uint64_t)n + TD - 1) / TD);
+    if (rank >= ntiles) return;  // workgroup-uniform
+    const uint32_t K = (ntiles - 1u - rank) / nwg + 1u;
+
+    uint4 pf[NP];  // planner: the descriptors of the tile it plans next
+    auto prefetch = [&](uint32_t k) {
+        const uint64_t t0 = (uint64_t)(rank + k * nwg) * TD;
+#pragma unroll
+        for (uint32_t p = 0; p < NP; ++p) {
+            const uint64_t i = t0 + p * 64u + lane;
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            typedef __attribute__((address_space(1))) const v4u gv4u;
+            v4u v = {0u, 0u, 0u, 0u};
+            if (i < n) v = *reinterpret_cast<gv4u*>(reinterpret_cast<uint64_t>(descs + i));
+            pf[p] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+    };
+    auto plan = [&](uint32_t k, WsBuf<TD>& b) {
+        const uint64_t t0 = (uint64_t)(rank + k * nwg) * TD;
+        for (uint32_t g = lane; g < FG; g += 64u) b.grp[g] = make_uint2(0u, 0u);
+        lds_sync();
+        uint32_t rk = 0, cc = 0, nb = 0;
+#pragma unroll
+        for (uint32_t p = 0; p < NP; ++p) {
+            const uint32_t j = p * 64u + lane;
+            const uint64_t i = t0 + j;
+            uint32_t nch = 0, meta = 0, fw = 0, start_sum = 0;
+            uint64_t a0 = 0;
+            bool big = false;
+            if (i < n) {
+                const uint64_t off = ((uint64_t)pf[p].y << 32) | pf[p].x;
+                const uint32_t len = pf[p].z;
+                start_sum = pf[p].w;
+                if ((int32_t)len > 0) {
+                    const uint64_t abs = reinterpret_cast<uint64_t>(base) + off;
+                    const bool odd = abs & 1ull;
+                    const uint32_t lo = (uint32_t)(abs & 15ull);
+                    const uint64_t span = (uint64_t)lo + len;
+                    const uint64_t c64 = (span + 15u) >> 4;
+                    const uint32_t lastv = (uint32_t)(span - 16ull * (c64 - 1u));
+                    big = c64 > FCAP;
+                    a0 = abs & ~15ull;
+                    nch = big ? 0u : (uint32_t)c64;
+                    const bool ef = !big && (lo != 0u || (c64 == 1u && lastv != 16u));
+                    const bool el = !big && c64 > 1u && lastv != 16u;
+                    const uint32_t fl = ((uint32_t)odd << 9) | ((uint32_t)ef << 10) | ((uint32_t)el << 11);
+                    meta = nch | fl | (j << 18);
+                    fw = nch | fl | (lo << 12) | (lastv << 16);
+                }
+            }
+            b.acc[j] = 0u;
+            b.fin[j] = make_uint2(start_sum, fw);
+            const uint32_t sa = (big ? 0x10000u : 0u) | (nch ? 1u : 0u);
+            const uint32_t ia = wave_incl_scan(sa), ib = wave_incl_scan(nch);
+            const uint32_t e1 = rk + ((ia - sa) & 0xffffu), cs = cc + ib - nch;
+            const uint32_t bp = nb + ((ia - sa) >> 16);
+            if (big) b.big[bp] = j;
+            if (nch) {
+                b.rec[e1] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), cs, meta);
+                const uint32_t g = cs >> 6, bit = cs & 63u;
+                if (bit < 32u) atomicOr(&b.grp[g].x, 1u << bit);
+                else atomicOr(&b.grp[g].y, 1u << (bit - 32u));
+                for (uint32_t gg = g + 1u; gg < FG && (gg << 6) <= cs + nch; ++gg) b.hb[gg] = (uint16_t)(e1 + 1u);
+            }
+            const uint32_t ta = uniform(__builtin_amdgcn_readlane(ia, 63)), tb = uniform(__builtin_amdgcn_readlane(ib, 63));
+            rk += ta & 0xffffu;
+            nb += ta >> 16;
+            cc += tb;
+        }
+        if (lane == 0u) {
+            b.hb[0] = 0;
+            b.C = cc;
+            b.nbig = nb;
+        }
+    };
+    auto finish_tile = [&](uint32_t k, WsBuf<TD>& b) {
+        const uint64_t t0 = (uint64_t)(rank + k * nwg) * TD;
+        const uint32_t nbig = uniform(b.nbig);
+        for (uint32_t q = 0; q < nbig; ++q) {
+            const uint32_t tq = uniform(b.big[q]);
+            const lvlip_csum_desc d = descs[t0 + tq];
+            const uint64_t abs = reinterpret_cast<uint64_t>(base) + d.offset;
+            const int lo = (int)(abs & 15ull);
+            const uint64_t span = (uint64_t)lo + (uint64_t)(uint32_t)d.len;
+            const uint32_t nchq = (uint32_t)((span + 15u) >> 4);
+            const uint32_t lastv = (uint32_t)(span - 16ull * (nchq - 1u));
+            const uint4* src = reinterpret_cast<const uint4*>(abs & ~15ull);
+            uint32_t w = (abs & 1ull) ? wave_packet_sum<4, true>(src, nchq, lo, lastv, lane)
+                                      : wave_packet_sum<4, false>(src, nchq, lo, lastv, lane);
+            w = wave_sum_dpp(w);
+            if (lane == 0) b.acc[tq] = w;
+        }
+        lds_sync();
+#pragma unroll
+        for (uint32_t p = 0; p < NP; ++p) {
+            const uint32_t j = p * 64u + lane;
+            const uint64_t i = t0 + j;
+            if (i < n) {
+                uint32_t acc = b.acc[j];
+                const uint2 f = b.fin[j];
+                const uint32_t m = f.y;
+                if (m & (3u << 10)) {
+                    const bool odd = m & (1u << 9);
+                    const int lo = (int)((m >> 12) & 15u), lastv = (int)(m >> 16);
+                    uint32_t c = 0;
+                    if (m & (1u << 10)) {
+                        uint4 e = b.edge[2u * j];
+                        const int fb1 = (m & 0xFFu) == 1u ? lastv : 16;
+                        e.x &= ~byte_range_mask(lo, fb1, 0);
+                        e.y &= ~byte_range_mask(lo, fb1, 1);
+                        e.z &= ~byte_range_mask(lo, fb1, 2);
+                        e.w &= ~byte_range_mask(lo, fb1, 3);
+                        c += odd ? chunk_words<true>(e) : chunk_words<false>(e);
+                    }
+                    if (m & (1u << 11)) {
+                        uint4 e = b.edge[2u * j + 1u];
+                        e.x &= ~byte_range_mask(0, lastv, 0);
+                        e.y &= ~byte_range_mask(0, lastv, 1);
+                        e.z &= ~byte_range_mask(0, lastv, 2);
+                        e.w &= ~byte_range_mask(0, lastv, 3);
+                        c += odd ? chunk_words<true>(e) : chunk_words<false>(e);
+                    }
+                    acc -= c;
+                }
+                out[i] = finish(f.x, acc);
+            }
+        }
+    };
+    // k_flat2's phase 2 over buffer b, the WS_SW sweepers
+    auto sweep = [&](WsBuf<TD>& b) {
+        const uint32_t C = uniform(b.C);
+        if (C == 0u) return;
+        const uint32_t G = (C + 63u) >> 6;
+        const uint32_t rstep = GORD == 1 ? (uint32_t)U : (uint32_t)WS_SW * U;
+        const uint32_t gper = (G + WS_SW - 1u) / WS_SW;
+        const uint32_t g_lo = GORD == 1 ? wid * gper : wid * (uint32_t)U;
+        const uint32_t g_end = GORD == 1 ? (g_lo + gper < G ? g_lo + gper : G) : G;
+        for (uint32_t gr = g_lo; gr < g_end; gr += rstep) {
+            uint4 x[U], rec[U];
+            uint32_t kk[U], hlo[U], hhi[U], hb[U];
+            bool vl[U], gv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t g = gr + u;
+                gv[u] = g < g_end;
+                const uint32_t gc = gv[u] ? g : G - 1u;
+                const uint2 gg = b.grp[gc];
+                hlo[u] = uniform(gg.x);
+                hhi[u] = uniform(gg.y);
+                hb[u] = uniform((uint32_t)b.hb[gc]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t H = ((uint64_t)hhi[u] << 32) | hlo[u];
+                const uint64_t Hs = H >> 1;
+                const uint32_t cnt = __builtin_amdgcn_mbcnt_hi((uint32_t)(Hs >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)Hs, 0u));
+                rec[u] = b.rec[(hb[u] + (uint32_t)(H & 1ull) - 1u) + cnt];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t j = (gr + u) * 64u + lane;
+                vl[u] = gv[u] && j < C;
+                kk[u] = vl[u] ? j - rec[u].z : 0u;
+                x[u] = load_nt_global((((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * kk[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!gv[u]) break;  // uniform
+                uint4 v = x[u];
+                const uint32_t m = rec[u].w;
+                if (__builtin_amdgcn_ballot_w64((m & (1u << 9)) != 0u)) {
+                    const uint32_t sel = (m & (1u << 9)) ? 0x02030001u : 0x03020100u;
+                    v.x = __builtin_amdgcn_perm(v.x, v.x, sel);
+                    v.y = __builtin_amdgcn_perm(v.y, v.y, sel);
+                    v.z = __builtin_amdgcn_perm(v.z, v.z, sel);
+                    v.w = __builtin_amdgcn_perm(v.w, v.w, sel);
+                }
+                uint32_t val = 0;
+                val = dot2_acc(v.x, val);
+                val = dot2_acc(v.y, val);
+                val = dot2_acc(v.z, val);
+                val = dot2_acc(v.w, val);
+                val = vl[u] ? val : 0u;
+                const uint32_t P = wave_incl_scan(val);
+                const bool first = kk[u] == 0u;
+                const bool last = kk[u] + 1u == (m & 0xFFu);
+                const uint32_t add = (first ? val - P : 0u) + ((last || lane == 63u) ? P : 0u);
+                if (vl[u] && (first || last || lane == 63u)) atomicAdd(&b.acc[m >> 18], add);
+                if (vl[u] && first && (m & (1u << 10))) b.edge[2u * (m >> 18)] = x[u];
+                if (vl[u] && last && (m & (1u << 11))) b.edge[2u * (m >> 18) + 1u] = x[u];
+            }
+        }
+    };
+
+    if (planner) {
+        prefetch(0);
+        plan(0, B[0]);
+    }
+    __syncthreads();
+    for (uint32_t k = 0; k < K; ++k) {
+        WsBuf<TD>& cur = B[k & 1u];
+        WsBuf<TD>& oth = B[(k & 1u) ^ 1u];
+        if (!planner) {
+            sweep(cur);
+        } else {
+            if (k + 1u < K) prefetch(k + 1u);
+            if (k >= 1u) finish_tile(k - 1u, oth);
+            if (k + 1u < K) {
+                lds_sync();
+                plan(k + 1u, oth);
+            }
+        }
+        __syncthreads();
+    }
+    if (planner) finish_tile(K - 1u, B[(K - 1u) & 1u]);
+}
+
 }  // namespace lvlip
 
 namespace {
@@ -1031,6 +1295,32 @@ bool launch_rflat(int u, int tile, int waves_per_cu, hipStream_t s, const void* 
     }
 }
 
+// k_wsflat: wgs_per_cu persistent workgroups on every CU (fewer when the batch
+// has fewer tiles), a multiple of 8 when it can (XCD-major ranks).
+template <int U, int TD, int GORD>
+void launch_wsflat_t(int wgs_per_cu, hipStream_t s, const void* base, const lvlip_csum_desc* d, uint32_t n,
+                     uint16_t* out) {
+    uint64_t grid = (uint64_t)lvlip_host::current_cus() * (uint64_t)wgs_per_cu;
+    const uint64_t nt = ((uint64_t)n + TD - 1) / TD;
+    if (grid > nt) grid = nt;
+    if (grid > 8) grid = grid & ~7ull;
+    hipLaunchKernelGGL((lvlip::k_wsflat<U, TD, GORD>), dim3((uint32_t)grid), dim3((lvlip::WS_SW + 1) * 64), 0, s,
+                       (const uint8_t*)base, d, n, out);
+}
+
+bool launch_wsflat(int u, int tile, int gord, int wgs_per_cu, hipStream_t s, const void* base,
+                   const lvlip_csum_desc* d, uint32_t n, uint16_t* out) {
+    switch ((u * 1000 + tile) * 4 + gord) {
+#define LVLIP_WS(UU, TT, GG) \
+    case (UU * 1000 + TT) * 4 + GG: launch_wsflat_t<UU, TT, GG>(wgs_per_cu, s, base, d, n, out); return true;
+        LVLIP_WS(4, 64, 1) LVLIP_WS(4, 128, 1) LVLIP_WS(4, 256, 1)
+        LVLIP_WS(8, 128, 1) LVLIP_WS(8, 256, 1) LVLIP_WS(8, 256, 2) LVLIP_WS(4, 256, 2)
+        LVLIP_WS(2, 64, 1) LVLIP_WS(2, 128, 1)
+#undef LVLIP_WS
+        default: return false;
+    }
+}
+
 int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uint16_t* out, hipStream_t s,
                  const lvlip_launch_cfg* cfg) {
     const int kernel = cfg ? cfg->kernel : -1;
@@ -1158,6 +1448,18 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             if (u == 0) u = 4;
             if (tile == 0) tile = 16;
             if (!launch_rflat(u, tile, wpc > 0 ? wpc : 12, s, base, descs, n, out)) return LVLIP_EINVAL;
+            break;
+        }
+        case 12: {
+            // unroll = group loads per round (low byte: 2, 4, 8; 0 = 4) |
+            // descriptors per tile / 64 << 8 (1, 2, 4; 0 = 4) | 1 << 12 for
+            // block group order (else quarters); 2 workgroups/CU by default
+            if (unroll < 0 || (unroll >> 13) != 0) return LVLIP_EINVAL;
+            int u = unroll & 0xff, tile = ((unroll >> 8) & 0xf) * 64;
+            if (u == 0) u = 4;
+            if (tile == 0) tile = 256;
+            const int gord = (unroll >> 12) & 1 ? 2 : 1;
+            if (!launch_wsflat(u, tile, gord, wpc > 0 ? wpc : 2, s, base, descs, n, out)) return LVLIP_EINVAL;
             break;
         }
         case 5: {  // first-generation flat kernel

@@ -64,6 +64,9 @@ VARIANTS = [
     (lvlip.KERNEL_RFLAT, 2 | (32 << 8), 1),
     (lvlip.KERNEL_RFLAT, 8 | (64 << 8), 16),
     (lvlip.KERNEL_RFLAT, 6 | (16 << 8), 4),
+    (lvlip.KERNEL_WSFLAT, 0, 0),   # sweeper waves + a planner wave, tiles double-buffered
+    (lvlip.KERNEL_WSFLAT, 2 | (1 << 8), 1),
+    (lvlip.KERNEL_WSFLAT, 8 | (4 << 8) | (1 << 12), 3),
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
@@ -237,6 +240,7 @@ def test_full_size_bit_exact(name):
                     (lvlip.KERNEL_WINDOW, 3, 0), (lvlip.KERNEL_WINDOW, 2, 0),
                     (lvlip.KERNEL_WFLAT, 0, 0), (lvlip.KERNEL_WFLAT, 8 | (64 << 8), 16),
                     (lvlip.KERNEL_RFLAT, 0, 0), (lvlip.KERNEL_RFLAT, 8 | (32 << 8), 8),
+                    (lvlip.KERNEL_WSFLAT, 0, 0), (lvlip.KERNEL_WSFLAT, 8 | (2 << 8), 3),
                     (lvlip.KERNEL_FLAT, 4 | (1 << 11), 0), (lvlip.KERNEL_FLAT, 8 | (1 << 11), 0),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
@@ -326,6 +330,34 @@ def test_rflat_tiles(shape):
             for wpc in (0, 1, 24):
                 out = lvlip.batch_torch(base, descs, kernel=lvlip.KERNEL_RFLAT, unroll=u | (tile << 8),
                                         waves_per_cu=wpc)
+                torch.cuda.synchronize()
+                got = out.cpu().numpy().view(np.uint16)
+                bad = np.nonzero(got != want[:n])[0]
+                assert bad.size == 0, (seed, n, wpc, bad[:5])
+
+
+# k_wsflat: every built (group loads per round, descriptors per tile, order)
+WSFLAT_SHAPES = [(4, 64, 0), (4, 128, 0), (4, 256, 0), (8, 128, 0), (8, 256, 0), (8, 256, 1), (4, 256, 1),
+                 (2, 64, 0), (2, 128, 0)]
+
+
+@pytest.mark.parametrize("shape", WSFLAT_SHAPES, ids=[f"u{u}d{d}b{b}" for u, d, b in WSFLAT_SHAPES])
+def test_wsflat_tiles(shape):
+    """k_wsflat for every built shape: batch sizes that leave the last tile
+    short or give workgroups no tile, 1 and 3 workgroups/CU (long per-workgroup
+    tile sequences through both LDS buffers, and workgroups with one tile:
+    plan, sweep and finish with nothing to overlap), ragged lengths with
+    descriptors past the sweep cap (the planner's big-packet loop), empty and
+    negative lengths at odd offsets, and tiny packets; every output against the
+    oracle."""
+    u, tile, blocks = shape
+    code = u | ((tile // 64) << 8) | (blocks << 12)
+    for seed, (base, d, want) in ((400 + u + tile, ragged_batch(400 + u + tile)),
+                                  (500 + u + tile, tiny_batch(500 + u + tile))):
+        for n in BATCH_SIZES:
+            descs = dev_descs(d[:n])
+            for wpc in (0, 1, 3):
+                out = lvlip.batch_torch(base, descs, kernel=lvlip.KERNEL_WSFLAT, unroll=code, waves_per_cu=wpc)
                 torch.cuda.synchronize()
                 got = out.cpu().numpy().view(np.uint16)
                 bad = np.nonzero(got != want[:n])[0]
@@ -451,7 +483,9 @@ def test_bad_launch_shapes_rejected():
                  (lvlip.KERNEL_LANE, 4 | (1 << 8) | (3 << 16)),
                  (lvlip.KERNEL_LANE, 4 | (1 << 8) | (1 << 25)),
                  (lvlip.KERNEL_RFLAT, 3), (lvlip.KERNEL_RFLAT, 2 | (64 << 8)), (lvlip.KERNEL_RFLAT, 4 | (48 << 8)),
-                 (lvlip.KERNEL_RFLAT, 4 | (1 << 16))):
+                 (lvlip.KERNEL_RFLAT, 4 | (1 << 16)),
+                 (lvlip.KERNEL_WSFLAT, 3), (lvlip.KERNEL_WSFLAT, 2 | (4 << 8)), (lvlip.KERNEL_WSFLAT, 4 | (3 << 8)),
+                 (lvlip.KERNEL_WSFLAT, 4 | (1 << 13))):
         with pytest.raises(lvlip.LvlipError):
             lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None, k, u, 0, 0)
 
@@ -468,7 +502,8 @@ def test_retired_and_lab_ids_rejected_by_the_product():
     L = lvlip.lib()
     for k, u in ((6, 0), (7, 0), (lvlip.KERNEL_WAVE, 2), (lvlip.KERNEL_WAVE_LDS, 2),
                  (lvlip.KERNEL_WAVE_SIMPLE, 2), (lvlip.KERNEL_FLAT_V1, 0), (lvlip.KERNEL_WFLAT, 0),
-                 (lvlip.KERNEL_FLAT, 6), (lvlip.KERNEL_FLAT, 4 | (2 << 8)), (lvlip.KERNEL_RFLAT, 0)):
+                 (lvlip.KERNEL_FLAT, 6), (lvlip.KERNEL_FLAT, 4 | (2 << 8)), (lvlip.KERNEL_RFLAT, 0),
+                 (lvlip.KERNEL_WSFLAT, 0)):
         cfg = lvlip.LaunchCfg(k, u, 0, 0)
         assert L.lvlip_csum_batch_dev_ex(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None,
                                          ctypes.byref(cfg)) == lvlip.EINVAL, (k, u)
@@ -717,7 +752,7 @@ def test_max_int_packet():
     for variant in [(lvlip.KERNEL_AUTO, 0, 0), (lvlip.KERNEL_WAVE, 2, 0), (lvlip.KERNEL_FLAT, 0, 0),
                     (lvlip.KERNEL_FLAT, 4 | (2 << 8), 0), (lvlip.KERNEL_WINDOW, 2 | (3 << 8), 0),
                     (lvlip.KERNEL_WINDOW, 3 | (1 << 8), 1), (lvlip.KERNEL_WFLAT, 0, 0),
-                    (lvlip.KERNEL_RFLAT, 0, 0),
+                    (lvlip.KERNEL_RFLAT, 0, 0), (lvlip.KERNEL_WSFLAT, 0, 0),
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_LANE, 0, 0), (lvlip.KERNEL_LANE, 2 | (4 << 8) | (1 << 16), 0)]:
         assert list(run(base, descs, variant)) == list(want), variant
