@@ -540,8 +540,13 @@ def run(args, world: int):
 
     kernel_label = f"{args.kernel}-u{args.unroll}-w{args.waves_per_cu}"
     chosen = args.kernel
-    if not args.dry_run and kernel == 0:
-        chosen = lvlip.auto_kernel_name(len_hint, b.n)
+    launches = 1
+    if not args.dry_run:
+        if kernel == 0:
+            chosen = lvlip.auto_kernel_name(len_hint, b.n)
+        # a step is one batch_dev call; long k_window batches go out as several
+        # launches (lvlip_batch_launches), and rocprof averages per launch
+        launches = max(1, lvlip.batch_launches(b.n, kernel, args.unroll, args.waves_per_cu, len_hint))
 
     diag = {"settle": {"launches": settle_n, "ms": round(settle_ms, 1)}}
     if verify is not None:
@@ -584,7 +589,9 @@ def run(args, world: int):
                          "traffic": traffic_from_profiles(args.workload, kernel_label,
                                                           KERNEL_FN.get(chosen, "")),
                          "kernel_ms": round(kern_ms, 5),
-                         "algo_bytes_per_launch": b.algo_bytes},
+                         "launches_per_step": launches,
+                         "kernel_ms_per_launch": round(kern_ms / launches, 5),
+                         "algo_bytes_per_launch": b.algo_bytes // launches},
             "cpu_baseline": cpu,
             "verified_bit_exact": verified,
             "dist": {"world_size": dist.get_world_size() if world > 1 else 1,

@@ -160,6 +160,14 @@ int lvlip_csum_batch_dev_ex(const void *base, const lvlip_csum_desc *descs,
  * waves_per_cu words and len_hint. */
 int lvlip_auto_kernel(int32_t len_hint, uint32_t n, lvlip_launch_cfg *resolved);
 
+/* How many kernel launches lvlip_csum_batch_dev_ex issues, back to back on
+ * its stream, for a batch of n descriptors with cfg (NULL = AUTO, resolved as
+ * the call resolves it) on the current HIP device: a WINDOW batch of more than
+ * ~120 packet groups per wave goes out in launches of ~80, any
+ * batch beyond 2^30 descriptors in launches of 2^30.  0 when n is 0 or above
+ * LVLIP_MAX_BATCH.  For profilers: per-launch figures are the batch's / this. */
+uint32_t lvlip_batch_launches(uint32_t n, const lvlip_launch_cfg *cfg);
+
 /* ======================================================================= */
 /* Group 3: host-resident batches (per-thread context)                      */
 /* ======================================================================= */

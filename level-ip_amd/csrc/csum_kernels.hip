@@ -525,6 +525,31 @@ constexpr uint64_t kWindowGroupsPerWave = 80;
 
 }  // namespace
 
+// Descriptors per launch for a batch of n with the resolved cfg c.
+static uint32_t launch_piece(const lvlip_launch_cfg& c, uint32_t n) {
+    // Long k_window launches lose rate: the persistent waves drift apart over
+    // a launch, and the window of the batch they read widens.  A batch of more
+    // than 1.5 x kWindowGroupsPerWave groups per wave goes out as launches of
+    // about kWindowGroupsPerWave groups per wave, back to back on the stream,
+    // which restart the waves in step (DESIGN.md §4; scripts/split_tune_once.sh:
+    // 8M MTU segments 6 725 GB/s in one launch, 6 866 in 8; 64M 6 450 in one,
+    // 6 850 in 64; 1M jumbo 7 113 in one, 7 146 in 2).  The configs' 1M MTU
+    // batch (85 groups per wave) stays one launch.  Results are the same bits:
+    // each launch checksums its own descriptor range.
+    uint32_t piece = kLaunchMax;
+    if (c.kernel == LVLIP_KERNEL_WINDOW) {
+        const int g = window_group((c.unroll >> 8) & 0xff, c.len_hint);
+        const uint64_t waves = (uint64_t)current_cus() * (uint64_t)(c.waves_per_cu > 0 ? c.waves_per_cu : 8);
+        const uint64_t per_launch = waves * (uint64_t)g * kWindowGroupsPerWave;
+        if ((uint64_t)n > per_launch + per_launch / 2u) {
+            const uint64_t parts = ((uint64_t)n + per_launch / 2u) / per_launch;
+            const uint64_t per = ((uint64_t)n + parts - 1) / parts;
+            if (per < piece) piece = (uint32_t)per;
+        }
+    }
+    return piece;
+}
+
 extern "C" {
 
 const char* lvlip_strerror(int err) {
@@ -549,6 +574,14 @@ int lvlip_device_count(void) {
     return c;
 }
 
+uint32_t lvlip_batch_launches(uint32_t n, const lvlip_launch_cfg* cfg) {
+    if (n == 0 || n > LVLIP_MAX_BATCH) return 0;
+    lvlip_launch_cfg c = cfg ? *cfg : lvlip_launch_cfg{LVLIP_KERNEL_AUTO, 0, 0, 0};
+    if (c.kernel == LVLIP_KERNEL_AUTO) c.kernel = auto_select(c.len_hint, n, &c.unroll, &c.waves_per_cu);
+    const uint32_t piece = launch_piece(c, n);
+    return (uint32_t)(((uint64_t)n + piece - 1) / piece);
+}
+
 int lvlip_auto_kernel(int32_t len_hint, uint32_t n, lvlip_launch_cfg* resolved) {
     int unroll = 0, wpc = 0;
     const int k = auto_select(len_hint, n, &unroll, &wpc);
@@ -569,26 +602,7 @@ int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* descs, uint
     // AUTO resolved once for the whole batch (its shape depends on n)
     lvlip_launch_cfg c = cfg ? *cfg : lvlip_launch_cfg{LVLIP_KERNEL_AUTO, 0, 0, 0};
     if (c.kernel == LVLIP_KERNEL_AUTO) c.kernel = auto_select(c.len_hint, n, &c.unroll, &c.waves_per_cu);
-    // Long k_window launches lose rate: the persistent waves drift apart over
-    // a launch, and the window of the batch they read widens.  A batch of more
-    // than 1.5 x kWindowGroupsPerWave groups per wave goes out as launches of
-    // about kWindowGroupsPerWave groups per wave, back to back on the stream,
-    // which restart the waves in step (DESIGN.md §4; scripts/split_tune_once.sh:
-    // 8M MTU segments 6 725 GB/s in one launch, 6 866 in 8; 64M 6 450 in one,
-    // 6 850 in 64; 1M jumbo 7 113 in one, 7 146 in 2).  The configs' 1M MTU
-    // batch (85 groups per wave) stays one launch.  Results are the same bits:
-    // each launch checksums its own descriptor range.
-    uint32_t piece = kLaunchMax;
-    if (c.kernel == LVLIP_KERNEL_WINDOW) {
-        const int g = window_group((c.unroll >> 8) & 0xff, c.len_hint);
-        const uint64_t waves = (uint64_t)current_cus() * (uint64_t)(c.waves_per_cu > 0 ? c.waves_per_cu : 8);
-        const uint64_t per_launch = waves * (uint64_t)g * kWindowGroupsPerWave;
-        if ((uint64_t)n > per_launch + per_launch / 2u) {
-            const uint64_t parts = ((uint64_t)n + per_launch / 2u) / per_launch;
-            const uint64_t per = ((uint64_t)n + parts - 1) / parts;
-            if (per < piece) piece = (uint32_t)per;
-        }
-    }
+    const uint32_t piece = launch_piece(c, n);
     for (uint32_t lo = 0; lo < n;) {
         const uint32_t m = n - lo < piece ? n - lo : piece;
         const int rc = dispatch_one(base, descs + lo, m, out + lo, (hipStream_t)stream, &c);

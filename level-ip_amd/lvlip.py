@@ -197,6 +197,7 @@ SIGNATURES = {
                                                 ctypes.c_void_p, ctypes.c_uint32]),
     "lvlip_tx_checksum_skb_list": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "lvlip_auto_kernel": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(LaunchCfg)]),
+    "lvlip_batch_launches": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.POINTER(LaunchCfg)]),
     "lvlip_build_id": (ctypes.c_char_p, []),
     "lvlip_abi_version": (ctypes.c_int, []),
     "lvlip_device_count": (ctypes.c_int, []),
@@ -300,6 +301,16 @@ def auto_kernel(len_hint: int, n: int) -> LaunchCfg:
     cfg = LaunchCfg()
     _lib.lvlip_auto_kernel(min(max(int(len_hint), 0), 0x7FFFFFFF), n, ctypes.byref(cfg))
     return cfg
+
+
+def batch_launches(n: int, kernel: int = KERNEL_AUTO, unroll: int = 0, waves_per_cu: int = 0,
+                   len_hint: int = 0) -> int:
+    """Kernel launches one batch_dev call of n descriptors issues with this
+    launch config (lvlip_batch_launches; AUTO resolved as the call does)."""
+    if is_lab_kernel(kernel, unroll):  # the lab launches 2^30 descriptors at most
+        return (n + (1 << 30) - 1) >> 30
+    cfg = LaunchCfg(kernel, unroll, waves_per_cu, min(max(int(len_hint), 0), 0x7FFFFFFF))
+    return int(_lib.lvlip_batch_launches(n, ctypes.byref(cfg)))
 
 
 def auto_kernel_name(len_hint: int, n: int) -> str:

@@ -490,6 +490,48 @@ def test_bad_launch_shapes_rejected():
             lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None, k, u, 0, 0)
 
 
+def test_batch_launches_reports_the_split():
+    """lvlip_batch_launches tells how many launches one batch_dev call issues
+    (what a profiler's per-launch average is per): the configs' 1M MTU batch is
+    one k_window launch, the 1M jumbo batch two (more than 120 groups per wave),
+    a 64M MTU batch one per ~80 groups per wave; FLAT and LANE batches one; the
+    lab's kernels one per 2^30 descriptors, any batch beyond 2^30 in launches
+    of 2^30; 0 for an empty or oversized batch.
+    And a batch AUTO splits checksums bit-exactly: 800 k short packets under
+    the jumbo hint (k_window's 9000-B shape, two launches) against the oracle."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert lvlip.batch_launches(0) == 0
+    assert lvlip.batch_launches(0xFFFFFFF1) == 0  # above LVLIP_MAX_BATCH
+    assert lvlip.batch_launches((1 << 30) + 1, lvlip.KERNEL_FLAT) == 2  # 2^30 per launch at most
+    assert lvlip.batch_launches(1 << 20, len_hint=1500) == 1
+    cfg = lvlip.auto_kernel(9000, 1 << 20)
+    assert cfg.kernel == lvlip.KERNEL_WINDOW
+    g = (cfg.unroll >> 8) & 0xFF or 3
+    per = cus * (cfg.waves_per_cu or 8) * g * 80
+    want = 1 if (1 << 20) <= per * 3 // 2 else ((1 << 20) + per // 2) // per
+    assert lvlip.batch_launches(1 << 20, len_hint=9000) == want >= 2
+    assert lvlip.batch_launches(64 << 20, len_hint=1500) >= 8
+    assert lvlip.batch_launches(1 << 20, lvlip.KERNEL_FLAT, len_hint=700) == 1
+    assert lvlip.batch_launches(1 << 20, len_hint=20) == 1
+    assert lvlip.batch_launches(1 << 20, lvlip.KERNEL_WSFLAT) == 1
+    n = 800_000
+    rng = np.random.default_rng(77)
+    host = rng.integers(0, 256, n * 64, dtype=np.uint8)
+    base = torch.from_numpy(host).cuda()
+    d = mk_descs(np.arange(n, dtype=np.uint64) * 64 + rng.integers(0, 8, n).astype(np.uint64),
+                 rng.integers(0, 56, n), rng.integers(0, 1 << 32, n, dtype=np.uint64))
+    want_out = pyoracle.batch(host, d, threads=THREADS)
+    descs = dev_descs(d)
+    hint = 9000  # k_window's jumbo shape on short packets: many groups per wave
+    k = lvlip.batch_launches(n, len_hint=hint)
+    assert k >= 2
+    out = lvlip.batch_torch(base, descs, len_hint=hint)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint16)
+    bad = np.nonzero(got != want_out)[0]
+    assert bad.size == 0, (k, bad[:5])
+
+
 def test_retired_and_lab_ids_rejected_by_the_product():
     """The product library runs AUTO, FLAT (2, 4, 8 loads per round), WINDOW and
     LANE only: the retired round-1 ids 6 and 7 and the lab's A/B ids return
