@@ -408,6 +408,86 @@ def test_lane_shapes(shape, mode):
         assert bad.size == 0, (n, bad[:5], [(int(d["offset"][i]), int(d["len"][i])) for i in bad[:5]])
 
 
+def _fuzz_batch(rng):
+    """A random batch: a mixture of length regimes (0-80 B, 81-2 000 B, MTU and
+    jumbo, up to 64 KiB, zero and negative), packed, overlapping or scattered
+    at any byte offset, random seeds (carry cases included)."""
+    n = int(rng.choice([1, 2, 5, 63, 64, 65, 255, 257, 1000, 4097, 20000, 60000]))
+    regime = rng.integers(0, 6)
+    if regime == 0:
+        ln = rng.integers(0, 81, n)
+    elif regime == 1:
+        ln = rng.integers(81, 2001, n)
+    elif regime == 2:
+        ln = rng.choice([1500, 1499, 9000, 8999, 20, 40, 60], n)
+    else:
+        r = rng.random(n)
+        ln = np.where(r < 0.4, rng.integers(0, 81, n), rng.integers(81, 3000, n))
+        big = rng.random(n) < 0.02
+        ln[big] = rng.integers(3000, 65536, int(big.sum()))
+    ln = ln.astype(np.int64)
+    ln[rng.random(n) < 0.01] = 0
+    ln[rng.random(n) < 0.005] = -int(rng.integers(1, 100))
+    layout = rng.integers(0, 3)
+    pos = np.maximum(ln, 0).astype(np.uint64)
+    if layout == 0:  # packed back to back from an odd start
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(pos[:-1])
+        off += np.uint64(rng.integers(0, 16))
+        size = int(off[-1] + pos[-1]) + 64
+    elif layout == 1:  # gaps of 0-40 B
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(pos[:-1] + rng.integers(0, 41, n - 1).astype(np.uint64))
+        off += np.uint64(rng.integers(0, 16))
+        size = int(off[-1] + pos[-1]) + 64
+    else:  # random, overlapping, in a small buffer
+        size = int(max(int(pos.max()) + 64, 1 << 20))
+        off = (rng.integers(0, size, n) % np.maximum(1, size - pos.astype(np.int64) - 1)).astype(np.uint64)
+    blob = rng.integers(0, 256, size, dtype=np.uint8)
+    if rng.random() < 0.3:  # runs of 0xff / 0x00 (fold edge cases)
+        a = int(rng.integers(0, size))
+        blob[a:a + int(rng.integers(0, 1 << 16))] = 0xFF if rng.random() < 0.5 else 0
+    st = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    st[rng.random(n) < 0.1] = 0xFFFFFFFF
+    return blob, mk_descs(off, ln, st)
+
+
+def _product_shapes(rng):
+    """A random launch the product library runs: AUTO with a random hint, FLAT
+    (U 2 / 4 / 8), WINDOW (pieces 2-4, G 1-4 or 8, 1-24 waves/CU), LANE (a
+    built shape, either load mode)."""
+    k = int(rng.integers(0, 4))
+    if k == 0:
+        return (lvlip.KERNEL_AUTO, 0, 0, int(rng.choice([0, 1, 20, 32, 33, 100, 500, 895, 896, 1500, 9000])))
+    if k == 1:
+        return (lvlip.KERNEL_FLAT, int(rng.choice([0, 2, 4, 8])), 0, 0)
+    if k == 2:
+        u = int(rng.choice([2, 3, 4])) | (int(rng.choice([0, 1, 2, 3, 4, 8])) << 8)
+        return (lvlip.KERNEL_WINDOW, u, int(rng.choice([0, 1, 4, 8, 12, 24])), 0)
+    sl, p, kk = LANE_SHAPES[int(rng.integers(0, len(LANE_SHAPES)))]
+    return (lvlip.KERNEL_LANE, p | (kk << 8) | (sl << 16) | (int(rng.integers(0, 2)) << 24), 0, 0)
+
+
+def test_random_batches_product_kernels():
+    """Randomized parity: 60 random batches (length regimes, layouts, offsets,
+    seeds, runs of 0x00 / 0xff) through random product launches (AUTO with
+    random hints, FLAT, WINDOW and LANE shapes), every output against the
+    oracle; the seed of a failing case is in the message."""
+    for case in range(60):
+        rng = np.random.default_rng(0xF022 + case)
+        blob, d = _fuzz_batch(rng)
+        want = pyoracle.batch(blob, d, threads=THREADS)
+        base = dev_blob(blob)
+        descs = dev_descs(d)
+        for _ in range(3):
+            k, u, w, h = _product_shapes(rng)
+            out = lvlip.batch_torch(base, descs, kernel=k, unroll=u, waves_per_cu=w, len_hint=h)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().view(np.uint16)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (case, (k, u, w, h), d.size, bad[:5])
+
+
 def test_auto_small_hints():
     """AUTO with small length hints (k_lane up to 32 B, the flat sweep above),
     on tiny packets next to long ones; against the oracle."""
