@@ -19,8 +19,9 @@
 //   k_rx_hdr  : the header-only RX frame call, one lane per frame.
 //   k_echo_reply : f4, the RFC 1624 echo reply of verified requests, one lane
 //               per frame.
-// The A/B variants measured against these (k_stream, k_wflat, the round-1
-// kernels, k_flat2's other shapes) live in liblvlip_lab.so (lab_kernels.hip).
+// The A/B variants measured against these (k_stream, k_wflat, k_rflat,
+// k_wsflat, the round-1 kernels, k_flat2's other shapes) live in
+// liblvlip_lab.so (lab_kernels.hip).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
