@@ -122,7 +122,7 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
 /* Kernel selection for lvlip_csum_batch_dev_ex.  AUTO picks by len_hint:
  * >= 896 B -> WINDOW (shape by the hint); 1-32 B -> LANE; otherwise or
  * unknown -> FLAT (measured: DESIGN.md §4-5).  lvlip_auto_kernel() tells
- * which kernel and shape AUTO runs.  Ids 1, 2, 4, 5, 6, 7, 9, 11, 12 are the A/B
+ * which kernel and shape AUTO runs.  Ids 1, 2, 4, 5, 6, 7, 9, 11-13 are the A/B
  * variants measured against these (liblvlip_lab.so, not this library): here
  * they return LVLIP_EINVAL. */
 #define LVLIP_KERNEL_AUTO        0  /* the default                                 */

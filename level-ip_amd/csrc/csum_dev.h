@@ -611,9 +611,10 @@ __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
 // plan's share of the launch (A/B, batch calls only; unroll bit 10).  Thread t
 // owns the tile's descriptors t*D .. t*D + D - 1, so its ranks, chunk starts
 // and big-packet slots follow from one exclusive scan of its D counts.
-template <int U, bool NT, int GORD, class Src, int D = 1, bool PIPE = false>
-__global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, const Src src,
-                                              uint32_t n) {
+// FIN_LDS (A/B, lab): phase 4's per-descriptor words go through LDS instead of
+// staying in registers across the sweep (fewer VGPRs live in phase 2).
+template <int U, bool NT, int GORD, class Src, int D = 1, bool PIPE = false, bool FIN_LDS = false>
+__device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, const Src src, uint32_t n) {
     static_assert(D == 1 || D == 2, "descriptors per thread");
     static_assert(!PIPE || (NT && U <= 8), "the pipelined sweep: nontemporal, at most 8 loads per round");
     constexpr uint32_t TD = (uint32_t)FT * D;   // descriptors per tile
@@ -625,6 +626,7 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
     __shared__ uint32_t s_big[TD];     // descriptors longer than FCAP chunks
     __shared__ uint4 s_edge[2 * TD];   // by descriptor: raw first / last chunk
     __shared__ uint32_t s_tmp[8];
+    __shared__ uint2 s_fin[FIN_LDS ? TD : 1];  // by descriptor: {start_sum, phase-4 word}
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t tile0 = blockIdx.x * TD;
@@ -698,6 +700,8 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
             }
         }
         s_acc[j] = wsum;
+        if constexpr (FIN_LDS)
+            s_fin[j] = make_uint2(start_sum[d], nch[d] | (meta[d] & (7u << 9)) | (lo[d] << 12) | (lastv[d] << 16));
     }
     for (uint32_t g = t; g < FG; g += FT) s_grp[g] = make_uint2(0u, 0u);
     // one scan pass for three prefixes: big packets (high half) and swept
@@ -957,6 +961,14 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
     for (int d = 0; d < D; ++d) {
         const uint32_t j = t * D + d, i = tile0 + j;
         uint16_t res = 0;
+        if constexpr (FIN_LDS) {
+            const uint2 f = s_fin[j];
+            start_sum[d] = f.x;
+            nch[d] = f.y & 0xFFu;
+            meta[d] = f.y & 0xFFFu;
+            lo[d] = (f.y >> 12) & 15u;
+            lastv[d] = f.y >> 16;
+        }
         if (i < n) {
             uint32_t acc = s_acc[j];
             if (meta[d] & (3u << 10)) {
@@ -985,6 +997,12 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
         }
         src.put(i, res, ctx[d], i < n, ent[d]);
     }
+}
+
+template <int U, bool NT, int GORD, class Src, int D = 1, bool PIPE = false>
+__global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, const Src src,
+                                              uint32_t n) {
+    flat2_body<U, NT, GORD, Src, D, PIPE>(base, src, n);
 }
 
 }  // namespace lvlip

@@ -12,6 +12,7 @@
 //                  round 3, DESIGN.md §4: instruction-bound, 4.0 vs 6.2 TB/s)
 //   k_wsflat       k_flat2's sweep in persistent workgroups of 4 sweeper
 //                  waves + 1 planner wave, tiles double-buffered (12)
+//   k_flat2_occ    k_flat2 compiled for a set number of waves per SIMD (13)
 //   k_flat2        its other shapes (3): group orders, tiles of 512, temporal
 //                  loads, U 6 / 12, an LDS pad; and the frame calls' variants
 //                  (8 loads per round, block order, plain field stores, the
@@ -1143,6 +1144,19 @@ __global__ __launch_bounds__((WS_SW + 1) * 64) void k_wsflat(const uint8_t* __re
     if (planner) finish_tile(K - 1u, B[(K - 1u) & 1u]);
 }
 
+
+// ------------------------------------------- k_flat2 at a set occupancy (13) --
+//
+// The product's k_flat2 (U loads per round, block order) compiled for at
+// least W waves per SIMD (amdgpu_waves_per_eu): U 8 takes 92 VGPRs, 5 waves
+// per SIMD = 5 workgroups per CU; W 6 caps it at 80 (6 workgroups).  The same
+// body (flat2_body), only the register budget differs.
+template <int U, int W, bool FIN>
+__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_flat2_occ(
+    const uint8_t* __restrict__ base, const DescSrc src, uint32_t n) {
+    flat2_body<U, true, 2, DescSrc, 1, false, FIN>(base, src, n);
+}
+
 }  // namespace lvlip
 
 namespace {
@@ -1460,6 +1474,24 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             if (tile == 0) tile = 256;
             const int gord = (unroll >> 12) & 1 ? 2 : 1;
             if (!launch_wsflat(u, tile, gord, wpc > 0 ? wpc : 2, s, base, descs, n, out)) return LVLIP_EINVAL;
+            break;
+        }
+        case 13: {
+            // k_flat2 at a set occupancy: unroll = loads per round (6, 8) |
+            // waves per SIMD << 8 (5, 6, 7) | 1 << 12 for phase 4's words in LDS
+            if (unroll < 0 || (unroll >> 13) != 0) return LVLIP_EINVAL;
+            const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
+            switch (unroll) {
+#define LVLIP_FOCC(UU, WW, FF)                                                                   \
+    case UU | (WW << 8) | (FF << 12):                                                            \
+        hipLaunchKernelGGL((lvlip::k_flat2_occ<UU, WW, FF>), dim3(grid), dim3(lvlip::FT), 0, s,  \
+                           (const uint8_t*)base, lvlip::DescSrc{descs, out}, n);                 \
+        break;
+                LVLIP_FOCC(8, 5, 0) LVLIP_FOCC(8, 5, 1) LVLIP_FOCC(8, 6, 0) LVLIP_FOCC(8, 6, 1)
+                LVLIP_FOCC(6, 7, 0) LVLIP_FOCC(6, 7, 1)
+#undef LVLIP_FOCC
+                default: return LVLIP_EINVAL;
+            }
             break;
         }
         case 5: {  // first-generation flat kernel

@@ -67,6 +67,9 @@ VARIANTS = [
     (lvlip.KERNEL_WSFLAT, 0, 0),   # sweeper waves + a planner wave, tiles double-buffered
     (lvlip.KERNEL_WSFLAT, 2 | (1 << 8), 1),
     (lvlip.KERNEL_WSFLAT, 8 | (4 << 8) | (1 << 12), 3),
+    (lvlip.KERNEL_FLAT_OCC, 8 | (5 << 8) | (1 << 12), 0),  # k_flat2 at a set occupancy
+    (lvlip.KERNEL_FLAT_OCC, 8 | (6 << 8), 0),
+    (lvlip.KERNEL_FLAT_OCC, 6 | (7 << 8) | (1 << 12), 0),
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
@@ -565,7 +568,9 @@ def test_bad_launch_shapes_rejected():
                  (lvlip.KERNEL_RFLAT, 3), (lvlip.KERNEL_RFLAT, 2 | (64 << 8)), (lvlip.KERNEL_RFLAT, 4 | (48 << 8)),
                  (lvlip.KERNEL_RFLAT, 4 | (1 << 16)),
                  (lvlip.KERNEL_WSFLAT, 3), (lvlip.KERNEL_WSFLAT, 2 | (4 << 8)), (lvlip.KERNEL_WSFLAT, 4 | (3 << 8)),
-                 (lvlip.KERNEL_WSFLAT, 4 | (1 << 13))):
+                 (lvlip.KERNEL_WSFLAT, 4 | (1 << 13)),
+                 (lvlip.KERNEL_FLAT_OCC, 8 | (7 << 8)), (lvlip.KERNEL_FLAT_OCC, 8 | (6 << 8) | (1 << 13)),
+                 (lvlip.KERNEL_FLAT_OCC, 0)):
         with pytest.raises(lvlip.LvlipError):
             lvlip.batch_dev(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None, k, u, 0, 0)
 
@@ -625,7 +630,7 @@ def test_retired_and_lab_ids_rejected_by_the_product():
     for k, u in ((6, 0), (7, 0), (lvlip.KERNEL_WAVE, 2), (lvlip.KERNEL_WAVE_LDS, 2),
                  (lvlip.KERNEL_WAVE_SIMPLE, 2), (lvlip.KERNEL_FLAT_V1, 0), (lvlip.KERNEL_WFLAT, 0),
                  (lvlip.KERNEL_FLAT, 6), (lvlip.KERNEL_FLAT, 4 | (2 << 8)), (lvlip.KERNEL_RFLAT, 0),
-                 (lvlip.KERNEL_WSFLAT, 0)):
+                 (lvlip.KERNEL_WSFLAT, 0), (lvlip.KERNEL_FLAT_OCC, 8 | (6 << 8))):
         cfg = lvlip.LaunchCfg(k, u, 0, 0)
         assert L.lvlip_csum_batch_dev_ex(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None,
                                          ctypes.byref(cfg)) == lvlip.EINVAL, (k, u)
