@@ -613,7 +613,15 @@ __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
 // and big-packet slots follow from one exclusive scan of its D counts.
 // FIN_LDS (A/B, lab): phase 4's per-descriptor words go through LDS instead of
 // staying in registers across the sweep (fewer VGPRs live in phase 2).
-template <int U, bool NT, int GORD, class Src, int D = 1, bool PIPE = false, bool FIN_LDS = false>
+// PFA (DescSrc only; the product's batch calls use kFlatPrefetchTiles): each
+// thread also loads the descriptor PFA tiles ahead of its own, issued after
+// its own (loads return in order, so its own descriptor's wait does not cover
+// it).  Block b runs on XCD b % 8 (as observed), so with PFA a multiple of 8
+// the workgroup that runs that tile later finds its descriptors in its own
+// XCD's L2: phase 1's first round trip becomes an L2 hit, and HBM traffic is
+// unchanged (PMC: FETCH_SIZE and L2 misses equal, L2 hits + the prefetch).
+template <int U, bool NT, int GORD, class Src, int D = 1, bool PIPE = false, bool FIN_LDS = false,
+          int PFA = 0>
 __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, const Src src, uint32_t n) {
     static_assert(D == 1 || D == 2, "descriptors per thread");
     static_assert(!PIPE || (NT && U <= 8), "the pipelined sweep: nontemporal, at most 8 loads per round");
@@ -633,6 +641,7 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
     const uint32_t t = tid;
 
     // ---- phase 1: descriptors -> chunk counts, ranks, records, head bitmap
+    uint4 pf = make_uint4(0u, 0u, 0u, 0u);  // PFA's prefetch, consumed at the end
     uint32_t start_sum[D], nch[D], meta[D], lo[D], lastv[D], ctx[D];
     uint64_t a0[D];  // the swept part's first chunk; its first byte is a0 + lo
     uint64_t ent[D];  // the entry's first byte (the frame calls' put)
@@ -653,6 +662,14 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
                 ds = src.get(i, ctx[d], win, &wa);
             else
                 ds = src.get(i, ctx[d]);
+            if constexpr (PFA > 0) {
+                if (d == 0) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    const uint64_t ip = (uint64_t)i + (uint64_t)PFA * TD;
+                    pf = load_global(reinterpret_cast<uint64_t>(src.descs + (ip < n ? ip : (uint64_t)i)));
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
             start_sum[d] = ds.start_sum;
             if (ds.len > 0) {
                 uint64_t abs = reinterpret_cast<uint64_t>(base) + ds.offset;
@@ -997,12 +1014,22 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
         }
         src.put(i, res, ctx[d], i < n, ent[d]);
     }
+    if constexpr (PFA > 0) {
+        // never true (n > 0): keeps the load and all four of its registers live
+        if ((pf.x ^ pf.y ^ pf.z ^ pf.w) == 0x5A5A5A5Au && n == 0u) s_tmp[0] = pf.y;
+    }
 }
 
-template <int U, bool NT, int GORD, class Src, int D = 1, bool PIPE = false>
+// The prefetch distance of the product's batch calls: the resident tiles of a
+// 256-CU MI355X (5 workgroups per CU at U 8).  Mixed, one process, 11 rounds:
+// 640 ahead +0.6 %, 1 280 +1.2 %, 2 560 +1.0 %, 4 480 +0.2 % over none
+// (profiles/r03_ab_flat_prefetch_mixed.json).
+constexpr int kFlatPrefetchTiles = 1280;
+
+template <int U, bool NT, int GORD, class Src, int D = 1, bool PIPE = false, int PFA = 0>
 __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, const Src src,
                                               uint32_t n) {
-    flat2_body<U, NT, GORD, Src, D, PIPE>(base, src, n);
+    flat2_body<U, NT, GORD, Src, D, PIPE, false, PFA>(base, src, n);
 }
 
 }  // namespace lvlip

@@ -471,19 +471,24 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             break;
         }
         case LVLIP_KERNEL_FLAT: {
-            // unroll = 64-chunk loads per round: 2, 4 or 8 (0 = 8: 94 VGPRs, 5
+            // unroll = 64-chunk loads per round: 2, 4 or 8 (0 = 8: 92 VGPRs, 5
             // workgroups per CU with 8 KiB in flight per wave, 2-3 % ahead of 4
-            // on mixed); groups in block order.  The other
-            // orders, tile sizes and load policies measured against it are
-            // lab variants (liblvlip_lab.so).
+            // on mixed); groups in block order; at U 8 each
+            // tile's threads prefetch the descriptors kFlatPrefetchTiles tiles
+            // ahead into their XCD's L2 (csum_dev.h; at U 2 / 4 the four
+            // registers it holds would cost a wave per SIMD, unmeasured).  The other orders, tile sizes,
+            // occupancies and load policies measured against it are lab
+            // variants (liblvlip_lab.so).
             if (unroll < 0) return LVLIP_EINVAL;
             if (unroll == 0) unroll = 8;
             const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
             switch (unroll) {
 #define LVLIP_FLAT(UU)                                                                         \
     case UU:                                                                                   \
-        hipLaunchKernelGGL((lvlip::k_flat2<UU, true, 2, lvlip::DescSrc>), dim3(grid), dim3(lvlip::FT), \
-                           0, s, (const uint8_t*)base, lvlip::DescSrc{descs, out}, n);        \
+        hipLaunchKernelGGL((lvlip::k_flat2<UU, true, 2, lvlip::DescSrc, 1, false,                \
+                                           UU == 8 ? lvlip::kFlatPrefetchTiles : 0>),             \
+                           dim3(grid), dim3(lvlip::FT), 0, s, (const uint8_t*)base,                \
+                           lvlip::DescSrc{descs, out}, n);                                        \
         break;
                 LVLIP_FLAT(2) LVLIP_FLAT(4) LVLIP_FLAT(8)
 #undef LVLIP_FLAT

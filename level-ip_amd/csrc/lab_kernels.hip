@@ -1151,10 +1151,10 @@ __global__ __launch_bounds__((WS_SW + 1) * 64) void k_wsflat(const uint8_t* __re
 // least W waves per SIMD (amdgpu_waves_per_eu): U 8 takes 92 VGPRs, 5 waves
 // per SIMD = 5 workgroups per CU; W 6 caps it at 80 (6 workgroups).  The same
 // body (flat2_body), only the register budget differs.
-template <int U, int W, bool FIN>
+template <int U, int W, bool FIN, int PFA = 0>
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_flat2_occ(
     const uint8_t* __restrict__ base, const DescSrc src, uint32_t n) {
-    flat2_body<U, true, 2, DescSrc, 1, false, FIN>(base, src, n);
+    flat2_body<U, true, 2, DescSrc, 1, false, FIN, PFA>(base, src, n);
 }
 
 }  // namespace lvlip
@@ -1478,10 +1478,19 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         }
         case 13: {
             // k_flat2 at a set occupancy: unroll = loads per round (6, 8) |
-            // waves per SIMD << 8 (5, 6, 7) | 1 << 12 for phase 4's words in LDS
-            if (unroll < 0 || (unroll >> 13) != 0) return LVLIP_EINVAL;
+            // waves per SIMD << 8 (5, 6, 7) | 1 << 12 for phase 4's words in
+            // LDS; or U 8, 5 waves with the descriptors of the tile P x 640
+            // ahead prefetched: 8 | 5 << 8 | P << 13 (P 1, 2, 4, 7)
+            if (unroll < 0 || (unroll >> 16) != 0) return LVLIP_EINVAL;
             const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
             switch (unroll) {
+#define LVLIP_FPF(PP)                                                                            \
+    case 8 | (5 << 8) | (PP << 13):                                                              \
+        hipLaunchKernelGGL((lvlip::k_flat2_occ<8, 5, false, PP * 640>), dim3(grid), dim3(lvlip::FT), 0, s, \
+                           (const uint8_t*)base, lvlip::DescSrc{descs, out}, n);                 \
+        break;
+                LVLIP_FPF(1) LVLIP_FPF(2) LVLIP_FPF(4) LVLIP_FPF(7)
+#undef LVLIP_FPF
 #define LVLIP_FOCC(UU, WW, FF)                                                                   \
     case UU | (WW << 8) | (FF << 12):                                                            \
         hipLaunchKernelGGL((lvlip::k_flat2_occ<UU, WW, FF>), dim3(grid), dim3(lvlip::FT), 0, s,  \

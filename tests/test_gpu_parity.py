@@ -70,6 +70,8 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT_OCC, 8 | (5 << 8) | (1 << 12), 0),  # k_flat2 at a set occupancy
     (lvlip.KERNEL_FLAT_OCC, 8 | (6 << 8), 0),
     (lvlip.KERNEL_FLAT_OCC, 6 | (7 << 8) | (1 << 12), 0),
+    (lvlip.KERNEL_FLAT_OCC, 8 | (5 << 8) | (1 << 13), 0),  # descriptors 640 tiles ahead prefetched
+    (lvlip.KERNEL_FLAT_OCC, 8 | (5 << 8) | (4 << 13), 0),
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
