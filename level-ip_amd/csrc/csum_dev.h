@@ -1032,6 +1032,73 @@ __global__ __launch_bounds__(FT) void k_flat2(const uint8_t* __restrict__ base, 
     flat2_body<U, NT, GORD, Src, D, PIPE, false, PFA>(base, src, n);
 }
 
+// --------------------------------------------- k_rx_hdr (RX header verify) --
+//
+// f1's header-only RX call (lvlip_rx_verify_dev without LVLIP_RX_VERIFY_L4) as
+// one lane per frame.  The parse window FrWin, here its first three chunks,
+// holds frame bytes [12, 45) at least: the whole IPv4 header for ihl 5-7, so
+// the lane sums it from registers (header dword m = window bytes 14+4m ..
+// 17+4m, one alignbyte each) and no entry, tile plan or second read of the
+// header exists.  Header words past the window (options) come from byte
+// loads.  The decisions are FrameSrc<FR_RX>'s (parse_rx) and the verdict
+// rule its put's.
+//
+// PFA > 0: each lane also loads the frame descriptor PFA blocks ahead, after
+// its own (as k_flat2's PFA), so that block's first round trip hits its XCD's
+// L2 (A/B in the lab, mode 3 of lvlip_lab_frames_dev).
+template <int PFA>
+__global__ __launch_bounds__(256) void k_rx_hdr(const uint8_t* __restrict__ base,
+                                                const lvlip_frame_desc* __restrict__ frames,
+                                                uint32_t n, uint8_t* __restrict__ verdict) {
+    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
+    if (f >= n) return;  // no cross-lane step below
+    const FrameSrc<FR_RX> src{base, nullptr, frames, verdict};
+    const uint4 raw = load_global(reinterpret_cast<uint64_t>(frames + f));
+    uint4 pf = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (PFA > 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t fp = (uint64_t)f + (uint64_t)PFA * 256u;
+        pf = load_global(reinterpret_cast<uint64_t>(frames + (fp < n ? fp : (uint64_t)f)));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    lvlip_frame_desc fd;
+    fd.offset = ((uint64_t)raw.y << 32) | raw.x;
+    fd.len = raw.z;
+    fd.reserved = 0;
+    const uint8_t* h = base + fd.offset;
+    // three chunks: frame bytes [12, cov), cov >= 45 (FrWin::load<3>), which
+    // hold every field parse_rx reads in this mode and the header of ihl 5-7
+    FrWin x;
+    x.load<3>(h, fd.len, reinterpret_cast<uint64_t>(frames + f) & ~15ull);
+    const uint32_t cov = 60u - (uint32_t)((reinterpret_cast<uint64_t>(h) + 12u) & 15u);
+    lvlip_csum_desc d0 = fr_mk(0, 0, 0), d1 = fr_mk(0, 0, 0);
+    uint32_t w = 0;
+    src.parse_rx(fd, x, d0, d1, w);
+    uint32_t v = w & 0xffu;
+    if (w & FR_HAS_HDR) {
+        const uint32_t ihl = x.b(14) & 0x0fu;
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t m = 0; m < 10u; ++m) {
+            // header dword m = frame bytes 14+4m .. 17+4m: from the window when
+            // it holds them, else from memory (options past the window)
+            const bool inw = 18u + 4u * m <= cov;
+            uint32_t hd = __builtin_amdgcn_alignbyte(x.A[m + 1u], x.A[m], 2u);
+            if (m < ihl && !inw) hd = fr_le16(h + 14u + 4u * m) | (fr_le16(h + 16u + 4u * m) << 16);
+            acc = dot2_acc(m < ihl ? hd : 0u, acc);
+        }
+        for (uint32_t k = 54u; k < FR_ETH + 4u * ihl; k += 2u) acc += fr_le16(h + k);
+        // src/ip_input.c:38-43, as FrameSrc<FR_RX>::put
+        if (finish(0u, acc) != 0u) v = LVLIP_RX_BAD_CSUM;
+        v = v == 0u ? (uint32_t)LVLIP_RX_OK : (v & ~FR_PENDING);
+    }
+    verdict[f] = (uint8_t)v;
+    if constexpr (PFA > 0) {
+        // never true (n > f): keeps the prefetch and its four registers live
+        if ((pf.x ^ pf.y ^ pf.z ^ pf.w) == 0x5A5A5A5Au && n == 0u) verdict[f] = (uint8_t)pf.y;
+    }
+}
+
 }  // namespace lvlip
 
 // ------------------------------------------------------------ host helpers --

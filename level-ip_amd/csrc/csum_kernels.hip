@@ -16,7 +16,7 @@
 //               that crosses packet boundaries; segment sums by a DPP prefix
 //               scan.  Also the frame calls' kernel (flat_src.h).
 //   k_lane    : up to 32 B (IPv4 headers alone): a few lanes per packet.
-//   k_rx_hdr  : the header-only RX frame call, one lane per frame.
+//   k_rx_hdr  : the header-only RX frame call, one lane per frame (csum_dev.h).
 //   k_echo_reply : f4, the RFC 1624 echo reply of verified requests, one lane
 //               per frame.
 // The A/B variants measured against these (k_stream, k_wflat, k_rflat,
@@ -166,57 +166,6 @@ __global__ __launch_bounds__(256) void k_lane(const uint8_t* __restrict__ base,
         const uint32_t i = i0 + PB * p;
         if (sub == 0u && i < n) out[i] = finish(dd[p].w, acc[p]);
     }
-}
-
-// --------------------------------------------- k_rx_hdr (RX header verify) --
-//
-// f1's header-only RX call (lvlip_rx_verify_dev without LVLIP_RX_VERIFY_L4) as
-// one lane per frame.  The parse window FrWin, here its first three chunks,
-// holds frame bytes [12, 45) at least: the whole IPv4 header for ihl 5-7, so
-// the lane sums it from registers (header dword m = window bytes 14+4m ..
-// 17+4m, one alignbyte each) and no entry, tile plan or second read of the
-// header exists.  Header words past the window (options) come from byte
-// loads.  The decisions are FrameSrc<FR_RX>'s (parse_rx) and the verdict
-// rule its put's.
-__global__ __launch_bounds__(256) void k_rx_hdr(const uint8_t* __restrict__ base,
-                                                const lvlip_frame_desc* __restrict__ frames,
-                                                uint32_t n, uint8_t* __restrict__ verdict) {
-    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
-    if (f >= n) return;  // no cross-lane step below
-    const FrameSrc<FR_RX> src{base, nullptr, frames, verdict};
-    const uint4 raw = load_global(reinterpret_cast<uint64_t>(frames + f));
-    lvlip_frame_desc fd;
-    fd.offset = ((uint64_t)raw.y << 32) | raw.x;
-    fd.len = raw.z;
-    fd.reserved = 0;
-    const uint8_t* h = base + fd.offset;
-    // three chunks: frame bytes [12, cov), cov >= 45 (FrWin::load<3>), which
-    // hold every field parse_rx reads in this mode and the header of ihl 5-7
-    FrWin x;
-    x.load<3>(h, fd.len, reinterpret_cast<uint64_t>(frames + f) & ~15ull);
-    const uint32_t cov = 60u - (uint32_t)((reinterpret_cast<uint64_t>(h) + 12u) & 15u);
-    lvlip_csum_desc d0 = fr_mk(0, 0, 0), d1 = fr_mk(0, 0, 0);
-    uint32_t w = 0;
-    src.parse_rx(fd, x, d0, d1, w);
-    uint32_t v = w & 0xffu;
-    if (w & FR_HAS_HDR) {
-        const uint32_t ihl = x.b(14) & 0x0fu;
-        uint32_t acc = 0;
-#pragma unroll
-        for (uint32_t m = 0; m < 10u; ++m) {
-            // header dword m = frame bytes 14+4m .. 17+4m: from the window when
-            // it holds them, else from memory (options past the window)
-            const bool inw = 18u + 4u * m <= cov;
-            uint32_t hd = __builtin_amdgcn_alignbyte(x.A[m + 1u], x.A[m], 2u);
-            if (m < ihl && !inw) hd = fr_le16(h + 14u + 4u * m) | (fr_le16(h + 16u + 4u * m) << 16);
-            acc = dot2_acc(m < ihl ? hd : 0u, acc);
-        }
-        for (uint32_t k = 54u; k < FR_ETH + 4u * ihl; k += 2u) acc += fr_le16(h + k);
-        // src/ip_input.c:38-43, as FrameSrc<FR_RX>::put
-        if (finish(0u, acc) != 0u) v = LVLIP_RX_BAD_CSUM;
-        v = v == 0u ? (uint32_t)LVLIP_RX_OK : (v & ~FR_PENDING);
-    }
-    verdict[f] = (uint8_t)v;
 }
 
 // ------------------------------------------ k_echo_reply (f4, RFC 1624) --
@@ -514,7 +463,7 @@ int launch_rx_hdr(const void* base, const lvlip_frame_desc* frames, uint32_t n, 
                   hipStream_t s) {
     for (uint32_t f0 = 0; f0 < n;) {
         const uint32_t m = n - f0 < kLaunchMax ? n - f0 : kLaunchMax;
-        hipLaunchKernelGGL(lvlip::k_rx_hdr, dim3((m + 255u) / 256u), dim3(256), 0, s,
+        hipLaunchKernelGGL(lvlip::k_rx_hdr<0>, dim3((m + 255u) / 256u), dim3(256), 0, s,
                            (const uint8_t*)base, frames + f0, m, out8 + f0);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "k_rx_hdr");

@@ -1536,8 +1536,10 @@ __attribute__((visibility("default"))) int lvlip_lab_batch_dev_ex(const void* ba
 
 // The frame calls' A/B variants on k_flat2 with a frame source.
 // mode: 0 TX fill, 1 RX header (the flat sweep instead of k_rx_hdr), 2 RX +
-// L4.  variant bits: 1 plain (temporal) TX field stores, 2 eight loads per
-// round, 4 block group order (else quarters).
+// L4; 3 the header-only call on k_rx_hdr with a descriptor prefetch.  variant
+// bits (modes 0-2): 1 plain (temporal) TX field stores, 2 eight loads per
+// round, 4 block group order (else quarters); mode 3: the prefetch distance
+// (variant >> 3) x 160 blocks.
 __attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int variant, void* base,
                                                                 const lvlip_frame_desc* frames, uint32_t n,
                                                                 uint8_t* out8, void* stream) {
@@ -1555,6 +1557,22 @@ __attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int va
         case 0: return LVLIP_LAB_FR(lvlip::FR_TX);
         case 1: return LVLIP_LAB_FR(lvlip::FR_RX);
         case 2: return LVLIP_LAB_FR(lvlip::FR_RX_L4);
+        case 3: {
+            // the header-only call on k_rx_hdr with its descriptor prefetch
+            // (variant >> 3) x 160 blocks ahead: 0, 1, 2, 4, 8
+            const uint32_t grid = (uint32_t)(((uint64_t)n + 255u) / 256u);
+            switch (variant >> 3) {
+#define LVLIP_RXH(P)                                                                               \
+    case P:                                                                                        \
+        hipLaunchKernelGGL(lvlip::k_rx_hdr<P * 160>, dim3(grid), dim3(256), 0, s, (const uint8_t*)base, \
+                           frames, n, out8);                                                       \
+        break;
+                LVLIP_RXH(0) LVLIP_RXH(1) LVLIP_RXH(2) LVLIP_RXH(4) LVLIP_RXH(8)
+#undef LVLIP_RXH
+                default: return LVLIP_EINVAL;
+            }
+            return hipGetLastError() == hipSuccess ? LVLIP_OK : LVLIP_EHIP;
+        }
         default: return LVLIP_EINVAL;
     }
 #undef LVLIP_LAB_FR
