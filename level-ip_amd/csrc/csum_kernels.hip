@@ -368,10 +368,12 @@ int auto_select(int hint, uint32_t n, int* unroll, int* wpc) {
         return LVLIP_KERNEL_LANE;
     }
     // below ~900 B the flat sweep leads (uniform 512 / 768 B: 6 442 / 6 482
-    // vs 3 973 / 5 916 GB/s for the stream), 4 loads per round below 320 B
-    // (64 / 128 B: 4 973 / 6 114 vs 3 825 / 5 448 with 8), 2 below 40 B, 8
-    // otherwise (mixed: 2-3 % ahead of 4)
-    if (*unroll <= 0) *unroll = (hint > 0 && hint < 40) ? 2 : (hint > 0 && hint < 320) ? 4 : 8;
+    // vs 3 973 / 5 916 GB/s for the stream), 4 loads per round below 176 B
+    // (64 / 128 / 160 B: 4 926 / 6 134 / 6 148 vs 3 984 / 5 723 / 5 806 with
+    // 8), 2 below 40 B, 8 otherwise (192 / 224 / 256 B: 6 340 / 6 387 / 6 348
+    // vs 6 225 / 6 226 / 6 273 with 4, since U 8's descriptor prefetch;
+    // mixed: 2-3 % ahead of 4)
+    if (*unroll <= 0) *unroll = (hint > 0 && hint < 40) ? 2 : (hint > 0 && hint < 176) ? 4 : 8;
     return LVLIP_KERNEL_FLAT;
 }
 

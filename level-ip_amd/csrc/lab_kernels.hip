@@ -1491,6 +1491,16 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         break;
                 LVLIP_FPF(1) LVLIP_FPF(2) LVLIP_FPF(4) LVLIP_FPF(7)
 #undef LVLIP_FPF
+                // U 4 (small-packet batches): 8 waves per SIMD without the
+                // prefetch (the product's U 4), 7 with it (4 more VGPRs)
+                case 4 | (8 << 8):
+                    hipLaunchKernelGGL((lvlip::k_flat2_occ<4, 8, false, 0>), dim3(grid), dim3(lvlip::FT), 0, s,
+                                       (const uint8_t*)base, lvlip::DescSrc{descs, out}, n);
+                    break;
+                case 4 | (7 << 8) | (2 << 13):
+                    hipLaunchKernelGGL((lvlip::k_flat2_occ<4, 7, false, 1280>), dim3(grid), dim3(lvlip::FT), 0,
+                                       s, (const uint8_t*)base, lvlip::DescSrc{descs, out}, n);
+                    break;
 #define LVLIP_FOCC(UU, WW, FF)                                                                   \
     case UU | (WW << 8) | (FF << 12):                                                            \
         hipLaunchKernelGGL((lvlip::k_flat2_occ<UU, WW, FF>), dim3(grid), dim3(lvlip::FT), 0, s,  \

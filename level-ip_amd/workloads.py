@@ -158,6 +158,10 @@ CONFIGS = {
 for _st in (1500, 1536, 2048):
     CONFIGS[f"tcp1500_s{_st}"] = (lambda st: lambda first=0, n=1 << 20: uniform(
         n, 1500, first, stride=st, name=f"tcp1500_s{st}"))(_st)
+# uniform small segments (~1.6 GB each) for the flat sweep's lab A/Bs
+for _ln in (64, 128, 160, 192, 224, 256, 512):
+    CONFIGS[f"tcp{_ln}"] = (lambda ln: lambda first=0, n=None: uniform(
+        n or (1600 << 20) // align16(ln), ln, first, name=f"tcp{ln}"))(_ln)
 
 
 def make(name: str, n: int | None = None, first: int = 0) -> Batch:

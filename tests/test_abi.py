@@ -105,3 +105,25 @@ def test_integration_index_names_every_declared_function():
     index = doc.split("## 6. Entry-point index", 1)[1]
     missing = [f for f in declared_functions() if f"`{f}`" not in index]
     assert not missing, missing
+
+
+def test_auto_selection_table():
+    """LVLIP_KERNEL_AUTO's choice by length hint (DESIGN.md §4's table), as
+    lvlip_auto_kernel reports it; no compute, so it runs without a GPU (the
+    window shapes assume 256 CUs there)."""
+    flat, window, lane = lvlip.KERNEL_FLAT, lvlip.KERNEL_WINDOW, lvlip.KERNEL_LANE
+    n = 1 << 20
+    for hint, kernel, unroll in ((0, flat, 8), (1, lane, 4 | (2 << 8) | (2 << 16)),
+                                 (32, lane, 4 | (2 << 8) | (2 << 16)), (33, flat, 2), (39, flat, 2),
+                                 (40, flat, 4), (175, flat, 4), (176, flat, 8), (391, flat, 8),
+                                 (895, flat, 8)):
+        cfg = lvlip.auto_kernel(hint, n)
+        assert (cfg.kernel, cfg.unroll) == (kernel, unroll), hint
+    for hint, wpc, g in ((896, 16, 4), (1500, 12, 4), (1792, 8, 2), (9000, 8, 3)):
+        cfg = lvlip.auto_kernel(hint, n)
+        assert cfg.kernel == window and cfg.waves_per_cu == wpc, hint
+        assert cfg.unroll == 2 | (g << 8), hint
+    # a batch launched as pieces: nothing for an empty one, one launch for a
+    # flat batch up to 2^30 descriptors
+    assert lvlip.batch_launches(0) == 0
+    assert lvlip.batch_launches(1 << 20, lvlip.KERNEL_FLAT, len_hint=391) == 1

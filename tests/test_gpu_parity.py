@@ -72,6 +72,7 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT_OCC, 6 | (7 << 8) | (1 << 12), 0),
     (lvlip.KERNEL_FLAT_OCC, 8 | (5 << 8) | (1 << 13), 0),  # descriptors 640 tiles ahead prefetched
     (lvlip.KERNEL_FLAT_OCC, 8 | (5 << 8) | (4 << 13), 0),
+    (lvlip.KERNEL_FLAT_OCC, 4 | (7 << 8) | (2 << 13), 0),
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
