@@ -620,8 +620,12 @@ __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
 // the workgroup that runs that tile later finds its descriptors in its own
 // XCD's L2: phase 1's first round trip becomes an L2 hit, and HBM traffic is
 // unchanged (PMC: FETCH_SIZE and L2 misses equal, L2 hits + the prefetch).
+// VAR (A/B bits, lab id 13): bit 0 raises the instruction-issue priority
+// (s_setprio 2) for the load-issuing part of each sweep round, bit 1 for phase
+// 1; bit 2 (block order) spreads a tile's last, partial round over the four
+// waves instead of leaving it to the first ones.
 template <int U, bool NT, int GORD, class Src, int D = 1, bool PIPE = false, bool FIN_LDS = false,
-          int PFA = 0>
+          int PFA = 0, int VAR = 0>
 __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, const Src src, uint32_t n) {
     static_assert(D == 1 || D == 2, "descriptors per thread");
     static_assert(!PIPE || (NT && U <= 8), "the pipelined sweep: nontemporal, at most 8 loads per round");
@@ -641,6 +645,7 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
     const uint32_t t = tid;
 
     // ---- phase 1: descriptors -> chunk counts, ranks, records, head bitmap
+    if constexpr ((VAR & 2) != 0) __builtin_amdgcn_s_setprio(2);
     uint4 pf = make_uint4(0u, 0u, 0u, 0u);  // PFA's prefetch, consumed at the end
     uint32_t start_sum[D], nch[D], meta[D], lo[D], lastv[D], ctx[D];
     uint64_t a0[D];  // the swept part's first chunk; its first byte is a0 + lo
@@ -756,6 +761,7 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
     }
     if (t == 0u) s_hb[0] = 0;
     __syncthreads();
+    if constexpr ((VAR & 2) != 0) __builtin_amdgcn_s_setprio(0);
 
     // ---- phase 2: sweep the chunk space, groups wid, wid+4, ... ; U per round.
     // Every round issues exactly U loads, unconditionally (lanes past the chunk
@@ -883,7 +889,24 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
             reduce(One{}, xb, mtb, kkb, vlb, gvb);
         }
     } else if (C > 0) {
-        for (uint32_t gr = g_lo; gr < g_end; gr += rstep) {
+        constexpr bool TAILB = (VAR & 4) != 0 && GORD == 2;
+        // TAILB: rr walks the workgroup's rounds; the last, partial one is
+        // dealt to the four waves in equal parts
+        for (uint32_t rr = TAILB ? 0u : g_lo; rr < g_end; rr += rstep) {
+            uint32_t gr = rr, ge = g_end;
+            if constexpr (TAILB) {
+                gr = rr + wid * (uint32_t)U;
+                if (rr + rstep > G) {
+                    const uint32_t R = G - rr;
+                    gr = rr + (R * wid) / 4u;
+                    ge = rr + (R * (wid + 1u)) / 4u;
+                }
+            }
+            if constexpr ((VAR & 1) != 0) {
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(2);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             uint4 x[U];
             uint32_t mt[U], kk[U];
             bool vl[U];
@@ -892,7 +915,7 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t g = gr + gstep * u;
-                gv[u] = g < g_end;
+                gv[u] = g < ge;
                 const uint32_t gc = gv[u] ? g : G - 1u;
                 const uint2 gg = s_grp[gc];
                 hlo[u] = uniform(gg.x);
@@ -921,6 +944,11 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
                 const uint64_t ca = (((uint64_t)rec[u].y << 32) | rec[u].x) + 16ull * kk[u];
                 x[u] = NT ? load_nt_global(ca) : load_global(ca);
                 mt[u] = rec[u].w;
+            }
+            if constexpr ((VAR & 1) != 0) {
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {

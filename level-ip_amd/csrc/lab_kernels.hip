@@ -1151,10 +1151,10 @@ __global__ __launch_bounds__((WS_SW + 1) * 64) void k_wsflat(const uint8_t* __re
 // least W waves per SIMD (amdgpu_waves_per_eu): U 8 takes 92 VGPRs, 5 waves
 // per SIMD = 5 workgroups per CU; W 6 caps it at 80 (6 workgroups).  The same
 // body (flat2_body), only the register budget differs.
-template <int U, int W, bool FIN, int PFA = 0>
+template <int U, int W, bool FIN, int PFA = 0, int VAR = 0>
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_flat2_occ(
     const uint8_t* __restrict__ base, const DescSrc src, uint32_t n) {
-    flat2_body<U, true, 2, DescSrc, 1, false, FIN, PFA>(base, src, n);
+    flat2_body<U, true, 2, DescSrc, 1, false, FIN, PFA, VAR>(base, src, n);
 }
 
 }  // namespace lvlip
@@ -1480,8 +1480,11 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             // k_flat2 at a set occupancy: unroll = loads per round (6, 8) |
             // waves per SIMD << 8 (5, 6, 7) | 1 << 12 for phase 4's words in
             // LDS; or U 8, 5 waves with the descriptors of the tile P x 640
-            // ahead prefetched: 8 | 5 << 8 | P << 13 (P 1, 2, 4, 7)
-            if (unroll < 0 || (unroll >> 16) != 0) return LVLIP_EINVAL;
+            // ahead prefetched: 8 | 5 << 8 | P << 13 (P 1, 2, 4, 7); the
+            // product's shape (P 2) with flat2_body's VAR bits Q (1 s_setprio
+            // 2 around the sweep's load issue, 2 around phase 1, 4 the last
+            // round dealt to all four waves): ... | Q << 16
+            if (unroll < 0 || (unroll >> 19) != 0) return LVLIP_EINVAL;
             const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
             switch (unroll) {
 #define LVLIP_FPF(PP)                                                                            \
@@ -1491,6 +1494,13 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         break;
                 LVLIP_FPF(1) LVLIP_FPF(2) LVLIP_FPF(4) LVLIP_FPF(7)
 #undef LVLIP_FPF
+#define LVLIP_FPR(QQ)                                                                            \
+    case 8 | (5 << 8) | (2 << 13) | (QQ << 16):                                                  \
+        hipLaunchKernelGGL((lvlip::k_flat2_occ<8, 5, false, 1280, QQ>), dim3(grid), dim3(lvlip::FT), 0, s, \
+                           (const uint8_t*)base, lvlip::DescSrc{descs, out}, n);                 \
+        break;
+                LVLIP_FPR(1) LVLIP_FPR(2) LVLIP_FPR(3) LVLIP_FPR(4) LVLIP_FPR(5) LVLIP_FPR(6) LVLIP_FPR(7)
+#undef LVLIP_FPR
                 // U 4 (small-packet batches): 8 waves per SIMD without the
                 // prefetch (the product's U 4), 7 with it (4 more VGPRs)
                 case 4 | (8 << 8):
