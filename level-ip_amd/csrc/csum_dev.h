@@ -623,7 +623,10 @@ __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
 // VAR (A/B bits, lab id 13): bit 0 raises the instruction-issue priority
 // (s_setprio 2) for the load-issuing part of each sweep round, bit 1 for phase
 // 1; bit 2 (block order) spreads a tile's last, partial round over the four
-// waves instead of leaving it to the first ones.
+// waves instead of leaving it to the first ones; bit 3 waits for every load
+// of a round (no early exit at the first group past the wave's); bit 5 is an
+// ablation (wrong results): the sweep's loads with one xor per dword instead
+// of the reduction.
 template <int U, bool NT, int GORD, class Src, int D = 1, bool PIPE = false, bool FIN_LDS = false,
           int PFA = 0, int VAR = 0>
 __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, const Src src, uint32_t n) {
@@ -889,6 +892,7 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
             reduce(One{}, xb, mtb, kkb, vlb, gvb);
         }
     } else if (C > 0) {
+        uint32_t abl = 0;  // VAR bit 5's ablation
         constexpr bool TAILB = (VAR & 4) != 0 && GORD == 2;
         // TAILB: rr walks the workgroup's rounds; the last, partial one is
         // dealt to the four waves in equal parts
@@ -952,7 +956,23 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                if (!gv[u]) break;  // uniform
+                if constexpr ((VAR & 32) != 0) {
+                    // ablation (A/B only, wrong results): the loads, every one
+                    // used unconditionally, without the reduction
+                    abl ^= x[u].x ^ x[u].y ^ x[u].z ^ x[u].w;
+                    continue;
+                }
+                // uniform.  VAR bit 3: no early exit, so no load of this round
+                // is left in flight into the next round's loop head (whose
+                // conservative wait would then also cover PFA's prefetch)
+                if (!gv[u]) {
+                    if constexpr ((VAR & 8) != 0) {
+                        asm volatile("" ::"v"(x[u].x));  // retire it here (vmcnt)
+                        continue;
+                    } else {
+                        break;
+                    }
+                }
                 uint4 v = x[u];
                 const uint32_t m = mt[u];
                 if (__builtin_amdgcn_ballot_w64((m & (1u << 9)) != 0u)) {
@@ -978,6 +998,7 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
                 if (vl[u] && last && (m & (1u << 11))) s_edge[2u * (m >> 18) + 1u] = x[u];
             }
         }
+        if constexpr ((VAR & 32) != 0) atomicAdd(&s_acc[t], abl);
     }
 
     // ---- phase 3: packets longer than FCAP chunks, one wave each

@@ -1483,8 +1483,9 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             // ahead prefetched: 8 | 5 << 8 | P << 13 (P 1, 2, 4, 7); the
             // product's shape (P 2) with flat2_body's VAR bits Q (1 s_setprio
             // 2 around the sweep's load issue, 2 around phase 1, 4 the last
-            // round dealt to all four waves): ... | Q << 16
-            if (unroll < 0 || (unroll >> 19) != 0) return LVLIP_EINVAL;
+            // round dealt to all four waves, 8 no early exit from a round, 32 the
+            // sweep's loads without the reduction: wrong results): ... | Q << 16
+            if (unroll < 0 || (unroll >> 22) != 0) return LVLIP_EINVAL;
             const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
             switch (unroll) {
 #define LVLIP_FPF(PP)                                                                            \
@@ -1499,7 +1500,7 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
         hipLaunchKernelGGL((lvlip::k_flat2_occ<8, 5, false, 1280, QQ>), dim3(grid), dim3(lvlip::FT), 0, s, \
                            (const uint8_t*)base, lvlip::DescSrc{descs, out}, n);                 \
         break;
-                LVLIP_FPR(1) LVLIP_FPR(2) LVLIP_FPR(3) LVLIP_FPR(4) LVLIP_FPR(5) LVLIP_FPR(6) LVLIP_FPR(7)
+                LVLIP_FPR(1) LVLIP_FPR(2) LVLIP_FPR(3) LVLIP_FPR(4) LVLIP_FPR(5) LVLIP_FPR(6) LVLIP_FPR(7) LVLIP_FPR(8) LVLIP_FPR(10) LVLIP_FPR(32)
 #undef LVLIP_FPR
                 // U 4 (small-packet batches): 8 waves per SIMD without the
                 // prefetch (the product's U 4), 7 with it (4 more VGPRs)

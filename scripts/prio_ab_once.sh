@@ -4,5 +4,5 @@ set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-AB_WORKLOAD=mixed AB_ROUNDS=9 AB_VARIANTS="${PRIO_VARIANTS:-auto:0:0,flat_occ:0x4508:0,flat_occ:0x14508:0,flat_occ:0x24508:0,flat_occ:0x34508:0,flat_occ:0x44508:0,flat_occ:0x54508:0}" timeout -k 10 240 python scripts/ab.py gpurun_out/prio_ab.json > gpurun_out/prio_ab.log 2>&1
+AB_WORKLOAD=mixed AB_ROUNDS=9 AB_VARIANTS="${PRIO_VARIANTS:-auto:0:0,flat_occ:0x4508:0,flat_occ:0x84508:0,flat_occ:0xA4508:0,flat_occ:0x24508:0}" timeout -k 10 240 python scripts/ab.py gpurun_out/prio_ab.json > gpurun_out/prio_ab.log 2>&1
 rc=$?; tail -8 gpurun_out/prio_ab.log; exit $rc
