@@ -674,7 +674,7 @@ __device__ __forceinline__ void flat2_body(const uint8_t* __restrict__ base, con
                 if (d == 0) {
                     __builtin_amdgcn_sched_barrier(0);
                     const uint64_t ip = (uint64_t)i + (uint64_t)PFA * TD;
-                    pf = load_global(reinterpret_cast<uint64_t>(src.descs + (ip < n ? ip : (uint64_t)i)));
+                    pf = load_global(reinterpret_cast<uint64_t>(src.desc_ptr(ip < n ? (uint32_t)ip : i)));
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }

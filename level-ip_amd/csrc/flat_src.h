@@ -40,6 +40,7 @@ struct DescSrc {
     __device__ __forceinline__ void put(uint32_t i, uint16_t c, uint32_t, bool valid, uint64_t) const {
         if (valid) out[i] = c;
     }
+    __device__ __forceinline__ const lvlip_csum_desc* desc_ptr(uint32_t i) const { return descs + i; }
 };
 
 // FrameSrc<MODE>: f1/f2 of SURVEY.md §8f on frames in HBM (include/lvlip_skb.h).

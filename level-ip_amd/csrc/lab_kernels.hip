@@ -1157,6 +1157,50 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
     flat2_body<U, true, 2, DescSrc, 1, false, FIN, PFA, VAR>(base, src, n);
 }
 
+// ------------------------------------- k_flat2 over a run-dealt tile map (14) --
+//
+// The product's k_flat2 U 8 (descriptor prefetch 1 280 tiles ahead), with
+// only the map from (block, tile slot) to descriptor changed.  The ~1 280
+// resident workgroups each stream their own ~100 KB tile, so together they
+// read a ~130 MB window of the batch at once; the window read probes are
+// fastest on narrow windows (k_window).  Here a generation of
+// NWG consecutive blocks shares a contiguous range of NWG x 256 descriptors,
+// dealt in runs of K: run k of block w's tile is the (k NWG + pos(w))-th run
+// of the generation, so workgroups that start together read neighbouring
+// runs (a window of NWG x K descriptors per run step).  XG: pos groups the
+// blocks of one XCD (block b runs on XCD b % 8) so that neighbouring runs,
+// which share edge lines, meet in one L2.  The last, partial generation keeps
+// the plain map.  A bijection on [0, n): results land where the product's do.
+template <int NWG, int K, bool XG>
+struct PermSrc {
+    static constexpr bool WIN_SUM = false;
+    static_assert(NWG % 8 == 0 && FT % K == 0, "generation of whole XCD groups, whole runs per tile");
+    const lvlip_csum_desc* descs;
+    uint16_t* out;
+    uint32_t n;
+    __device__ __forceinline__ uint32_t perm(uint32_t i) const {
+        constexpr uint32_t GEN = (uint32_t)NWG * FT;  // descriptors per generation
+        const uint32_t g = i / GEN;
+        if ((uint64_t)(g + 1u) * GEN > n) return i;  // last, partial generation
+        const uint32_t b = (i % GEN) / FT, j = i % FT;
+        const uint32_t pos = XG ? (b % 8u) * (NWG / 8u) + b / 8u : b;
+        return g * GEN + (j / K) * ((uint32_t)NWG * K) + pos * K + j % K;
+    }
+    __device__ __forceinline__ lvlip_csum_desc get(uint32_t i, uint32_t& ctx) const {
+        return DescSrc{descs, out}.get(perm(i), ctx);
+    }
+    __device__ __forceinline__ void put(uint32_t i, uint16_t c, uint32_t, bool valid, uint64_t) const {
+        if (valid) out[perm(i)] = c;
+    }
+    __device__ __forceinline__ const lvlip_csum_desc* desc_ptr(uint32_t i) const { return descs + perm(i); }
+};
+
+template <int NWG, int K, bool XG>
+__global__ __launch_bounds__(FT) void k_flat2_perm(const uint8_t* __restrict__ base, const PermSrc<NWG, K, XG> src,
+                                                   uint32_t n) {
+    flat2_body<8, true, 2, PermSrc<NWG, K, XG>, 1, false, false, 1280>(base, src, n);
+}
+
 }  // namespace lvlip
 
 namespace {
@@ -1520,6 +1564,25 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
                 LVLIP_FOCC(8, 5, 0) LVLIP_FOCC(8, 5, 1) LVLIP_FOCC(8, 6, 0) LVLIP_FOCC(8, 6, 1)
                 LVLIP_FOCC(6, 7, 0) LVLIP_FOCC(6, 7, 1)
 #undef LVLIP_FOCC
+                default: return LVLIP_EINVAL;
+            }
+            break;
+        }
+        case 14: {
+            // k_flat2 U 8 over the run-dealt tile map: unroll = run length K
+            // (8, 16, 32, 64) | generation / 640 blocks << 8 (1, 2, 4) | 1 << 12
+            // to group each XCD's blocks
+            if (unroll < 0 || (unroll >> 13) != 0) return LVLIP_EINVAL;
+            const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FT - 1) / lvlip::FT);
+            switch (unroll) {
+#define LVLIP_FPM(KK, GG, XX)                                                                          \
+    case KK | (GG << 8) | (XX << 12):                                                                  \
+        hipLaunchKernelGGL((lvlip::k_flat2_perm<GG * 640, KK, XX>), dim3(grid), dim3(lvlip::FT), 0, s,    \
+                           (const uint8_t*)base, lvlip::PermSrc<GG * 640, KK, XX>{descs, out, n}, n);  \
+        break;
+                LVLIP_FPM(8, 2, 1) LVLIP_FPM(16, 2, 1) LVLIP_FPM(32, 2, 1) LVLIP_FPM(64, 2, 1)
+                LVLIP_FPM(16, 2, 0) LVLIP_FPM(16, 1, 1) LVLIP_FPM(16, 4, 1) LVLIP_FPM(32, 1, 1)
+#undef LVLIP_FPM
                 default: return LVLIP_EINVAL;
             }
             break;
