@@ -73,6 +73,10 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT_OCC, 8 | (5 << 8) | (1 << 13), 0),  # descriptors 640 tiles ahead prefetched
     (lvlip.KERNEL_FLAT_OCC, 8 | (5 << 8) | (4 << 13), 0),
     (lvlip.KERNEL_FLAT_OCC, 4 | (7 << 8) | (2 << 13), 0),
+    (lvlip.KERNEL_FLAT_OCC, 0x4508 | (3 << 16), 0),  # + s_setprio around load issue and phase 1
+    (lvlip.KERNEL_FLAT_OCC, 0x4508 | (4 << 16), 0),  # + last round dealt to all four waves
+    (lvlip.KERNEL_FLAT_OCC, 0x4508 | (8 << 16), 0),  # + no early exit from a round
+    (lvlip.KERNEL_FLAT_PERM, 16 | (2 << 8) | (1 << 12), 0),  # run-dealt tile map (identity below a generation)
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
@@ -251,7 +255,16 @@ def test_full_size_bit_exact(name):
                     (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
                     (lvlip.KERNEL_FLAT, 8 | (1 << 10), 0),
-                    (lvlip.KERNEL_LANE, 0, 0), (lvlip.KERNEL_AUTO, 0, 0)]:
+                    (lvlip.KERNEL_LANE, 0, 0), (lvlip.KERNEL_AUTO, 0, 0),
+                    # lab A/B variants of round 3: VAR bits of k_flat2_occ, and the
+                    # run-dealt tile maps (full generations of 640-1 280 x 256 here)
+                    (lvlip.KERNEL_FLAT_OCC, 0x4508 | (3 << 16), 0),
+                    (lvlip.KERNEL_FLAT_OCC, 0x4508 | (4 << 16), 0),
+                    (lvlip.KERNEL_FLAT_OCC, 0x4508 | (8 << 16), 0),
+                    (lvlip.KERNEL_FLAT_PERM, 16 | (2 << 8) | (1 << 12), 0),
+                    (lvlip.KERNEL_FLAT_PERM, 16 | (2 << 8), 0),
+                    (lvlip.KERNEL_FLAT_PERM, 32 | (1 << 8) | (1 << 12), 0),
+                    (lvlip.KERNEL_FLAT_PERM, 64 | (2 << 8) | (1 << 12), 0)]:
         assert np.array_equal(run(base, descs, variant, out), want), variant
     # adversarial packets really are there and fold as the reference does
     ones = b.paint == 2
