@@ -4,7 +4,8 @@
 hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950 FETCH_SIZE
 reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read
 (MI355X_MICROARCH.md, HBM); WRITE_SIZE is taken as reported (2-B result stores,
-uncalibrated, ~0.1 % of the traffic).  Also copies the kernel-trace stats csv."""
+uncalibrated, ~0.1 % of the traffic).  Also copies the PMC run's kernel-trace stats csv (as <tag>_<workload>_pmc_run_kernel_stats.csv,
+not over the full command's trace summary)."""
 import csv
 import json
 import os
@@ -47,5 +48,8 @@ rec = {"tag": tag, "kernels": [{
 os.makedirs("profiles", exist_ok=True)
 out = f"profiles/{tag}_pmc_{workload}.json"
 json.dump(rec, open(out, "w"), indent=1)
-shutil.copy(os.path.join(prof, "trace", "trace_kernel_stats.csv"), f"profiles/{tag}_{workload}_kernel_stats.csv")
+# the short PMC run's own trace summary; profiles/<tag>_<workload>_kernel_stats.csv
+# is the full bench command's trace (scripts/evidence.sh step 2), kept apart
+shutil.copy(os.path.join(prof, "trace", "trace_kernel_stats.csv"),
+            f"profiles/{tag}_{workload}_pmc_run_kernel_stats.csv")
 print(out, json.dumps(rec["kernels"][0], indent=None)[:400])
