@@ -294,16 +294,16 @@ __device__ __forceinline__ void piece_wait(u32x4& a, u32x4& b) {
 // is owned by exactly one wave whatever the placement): neighbouring groups then
 // belong to waves of one XCD, so the partial 32-B sectors of their 2-B results
 // merge in that XCD's L2 before they are written back.
-template <int G>
+template <int G, int WPB = SW_WAVES>  // WPB: waves per workgroup
 struct Deal {
     uint64_t nw, rank, p_lo;
     uint32_t cnt;  // the wave's packets
 
     // false when this wave has no packet
     __device__ __forceinline__ bool init(uint32_t n, uint32_t wid) {
-        nw = (uint64_t)gridDim.x * SW_WAVES;
+        nw = (uint64_t)gridDim.x * WPB;
         if (G == 0) {
-            rank = (uint64_t)blockIdx.x * SW_WAVES + wid;
+            rank = (uint64_t)blockIdx.x * WPB + wid;
             const uint64_t per = ((uint64_t)n + nw - 1) / nw;
             p_lo = rank * per;
             if (p_lo >= n) return false;
@@ -311,8 +311,8 @@ struct Deal {
             return true;
         }
         rank = (gridDim.x & 7u) == 0u
-                   ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * SW_WAVES + wid
-                   : (uint64_t)blockIdx.x * SW_WAVES + wid;
+                   ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * WPB + wid
+                   : (uint64_t)blockIdx.x * WPB + wid;
         p_lo = 0;
         // gcount groups, the last one short when it is the batch's last
         const uint64_t ng = ((uint64_t)n + G - 1) / G;
@@ -331,9 +331,9 @@ struct Deal {
 
 // Descriptors of the wave's packets [first, first + 64) into an LDS window by
 // LDS-DMA, one per lane; issued from asm so hipcc does not see it in flight.
-template <int G>
+template <int G, int WPB>
 __device__ __forceinline__ void fetch_window(const lvlip_csum_desc* __restrict__ descs,
-                                             const Deal<G>& dl, uint32_t first, uint32_t lane,
+                                             const Deal<G, WPB>& dl, uint32_t first, uint32_t lane,
                                              uint4* win /* LDS, 64 entries */) {
     uint32_t k = first + lane;
     k = k < dl.cnt ? k : dl.cnt - 1u;  // lanes past the wave's packets re-read a valid descriptor
@@ -353,7 +353,7 @@ __device__ __forceinline__ void fetch_window(const lvlip_csum_desc* __restrict__
 #pragma clang diagnostic pop
 }
 
-template <int R, int G, int POL>
+template <int R, int G, int POL, int WPB = SW_WAVES>
 __device__ __forceinline__ void ring_sweep(const uint8_t* __restrict__ base,
                                            const lvlip_csum_desc* __restrict__ descs, uint32_t n,
                                            uint16_t* __restrict__ out, uint4 (*s_win)[64]) {
@@ -362,13 +362,13 @@ __device__ __forceinline__ void ring_sweep(const uint8_t* __restrict__ base,
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t lane16 = lane * 16u;
     const uint32_t wid = uniform(threadIdx.x >> 6);
-    Deal<G> dl;
+    Deal<G, WPB> dl;
     if (!dl.init(n, wid)) return;
     const uint32_t cnt = dl.cnt;
 
     // descriptor windows: the wave's packets [64w, 64w + 64) live in s_win[w & 1]
-    fetch_window<G>(descs, dl, 0u, lane, s_win[0]);
-    fetch_window<G>(descs, dl, 64u, lane, s_win[1]);
+    fetch_window<G, WPB>(descs, dl, 0u, lane, s_win[0]);
+    fetch_window<G, WPB>(descs, dl, 64u, lane, s_win[1]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // Packet metadata for the issue cursor's window, one packet per lane (VALU,
@@ -430,7 +430,7 @@ __device__ __forceinline__ void ring_sweep(const uint8_t* __restrict__ base,
                 if (ip < cnt) {
                     if ((ip & 63u) == 0u) {  // entered window ip/64
                         load_window_meta(ip >> 6);
-                        fetch_window<G>(descs, dl, ip + 64u, lane, s_win[((ip >> 6) + 1u) & 1u]);
+                        fetch_window<G, WPB>(descs, dl, ip + 64u, lane, s_win[((ip >> 6) + 1u) & 1u]);
                     }
                     pull(ip & 63u);
                 }

@@ -1195,6 +1195,31 @@ struct PermSrc {
     __device__ __forceinline__ const lvlip_csum_desc* desc_ptr(uint32_t i) const { return descs + perm(i); }
 };
 
+// ------------------------------------ k_window with per-wave time stamps --
+//
+// Diagnostic (lvlip_lab_window_stamps): the product's k_window body, each wave
+// stamping the real-time counter (100 MHz) when it starts and when its ring has
+// drained, into a buffer of its own (two u64 per wave rank, XCD-major ranks as
+// the deal uses).  Shows the launch's ramp (spread of start times) and tail
+// (spread of end times).  The stamps go nowhere else.
+template <int R, int G, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_window_stamp(const uint8_t* __restrict__ base,
+                                                           const lvlip_csum_desc* __restrict__ descs, uint32_t n,
+                                                           uint16_t* __restrict__ out, uint64_t* __restrict__ stamps) {
+    __shared__ uint4 s_win[WPB][2][64];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t wid = uniform(threadIdx.x >> 6);
+    ring_sweep<R, G, 0, WPB>(base, descs, n, out, s_win[wid]);
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t rank = (gridDim.x & 7u) == 0u
+                              ? ((uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * WPB + wid
+                              : (uint64_t)blockIdx.x * WPB + wid;
+    if ((threadIdx.x & 63u) == 0u) {
+        stamps[2 * rank] = t0;
+        stamps[2 * rank + 1] = t1;
+    }
+}
+
 template <int NWG, int K, bool XG>
 __global__ __launch_bounds__(FT) void k_flat2_perm(const uint8_t* __restrict__ base, const PermSrc<NWG, K, XG> src,
                                                    uint32_t n) {
@@ -1601,6 +1626,40 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
 }  // namespace
 
 extern "C" {
+
+// k_window R 2, G 4 (the MTU shape) at waves_per_cu waves on every CU, with
+// per-wave start/end stamps (2 u64 per wave) into `stamps`; returns the number
+// of waves (stamps needs 16 B each), or a negative LVLIP_E*.
+// wpb: waves per workgroup (4, 8 or 12): with wpb = waves_per_cu every CU runs
+// one workgroup.
+__attribute__((visibility("default"))) int lvlip_lab_window_stamps(const void* base, const lvlip_csum_desc* descs,
+                                                                   uint32_t n, uint16_t* out, uint64_t* stamps,
+                                                                   uint64_t stamp_bytes, int waves_per_cu, int wpb,
+                                                                   void* stream) {
+    if (!base || !descs || !out || !stamps || n == 0 || waves_per_cu <= 0) return LVLIP_EINVAL;
+    if (wpb != 4 && wpb != 8 && wpb != 12) return LVLIP_EINVAL;
+    uint64_t waves = (uint64_t)lvlip_host::current_cus() * (uint64_t)waves_per_cu;
+    const uint64_t ng = ((uint64_t)n + 3) / 4;
+    if (waves > ng) waves = ng;
+    uint64_t grid = (waves + wpb - 1) / wpb;
+    if (grid > 8) grid = grid & ~7ull;
+    if (grid * wpb * 16ull > stamp_bytes) return LVLIP_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    switch (wpb) {
+        case 4:
+            hipLaunchKernelGGL((lvlip::k_window_stamp<2, 4, 4>), dim3((uint32_t)grid), dim3(256), 0, s,
+                               (const uint8_t*)base, descs, n, out, stamps);
+            break;
+        case 8:
+            hipLaunchKernelGGL((lvlip::k_window_stamp<2, 4, 8>), dim3((uint32_t)grid), dim3(512), 0, s,
+                               (const uint8_t*)base, descs, n, out, stamps);
+            break;
+        default:
+            hipLaunchKernelGGL((lvlip::k_window_stamp<2, 4, 12>), dim3((uint32_t)grid), dim3(768), 0, s,
+                               (const uint8_t*)base, descs, n, out, stamps);
+    }
+    return hipGetLastError() == hipSuccess ? (int)(grid * wpb) : LVLIP_EHIP;
+}
 
 // lvlip_csum_batch_dev_ex's contract for the lab kernel ids (1, 2, 3, 4, 5, 9, 11).
 __attribute__((visibility("default"))) int lvlip_lab_batch_dev_ex(const void* base,

@@ -71,14 +71,16 @@ def stream_kernels(asm):
     assert st == {(r, p) for r in (2, 3, 4) for p in range(5)}, sorted(st)
     # k_window<R, G>: every pieces-in-flight x group-size pair the launcher uses
     win = {tuple(int(x) for x in re.search(r"k_windowILi(\d+)ELi(\d+)E", n).groups())
-           for n in ks if "k_window" in n}
+           for n in ks if "k_windowI" in n}
+    # the lab's stamped k_window (same ring, 4 / 8 / 12 waves per workgroup)
+    assert any("k_window_stamp" in n for n in ks)
     assert win == {(r, g) for r in (2, 3, 4) for g in (1, 2, 3, 4, 8)}, sorted(win)
     return ks
 
 
 def pieces(name):
     """R (pieces in flight) of a k_stream / k_window instantiation."""
-    return int(re.search(r"k_(?:stream|window)ILi(\d+)E", name).group(1))
+    return int(re.search(r"k_(?:stream|window|window_stamp)ILi(\d+)E", name).group(1))
 
 
 def test_buffer_loads_padded_against_valu_sgpr_hazard(asm):
