@@ -1195,6 +1195,245 @@ struct PermSrc {
     __device__ __forceinline__ const lvlip_csum_desc* desc_ptr(uint32_t i) const { return descs + perm(i); }
 };
 
+// -------------------------- k_window_dyn: the window deal, balanced in the CU --
+//
+// lab_tail.py's stamps show k_window's waves ending ~25 us apart on tcp1500,
+// the same waves late in every launch, and the spread inside each CU (the
+// waves sharing a CU end ~10 us apart whatever the workgroup shape).  Here one
+// workgroup of WPB waves runs per CU and owns the groups of its WPB ranks of
+// the window deal, item i = (j = i / WPB, r = i % WPB) -> group
+// j * nw + bx * WPB + r (bx: XCD-major block order).  Each wave's first two
+// descriptor windows take its static items (j < 2 * 64/G, r = wave), as
+// k_window would; after that a wave claims one item per group from an LDS
+// counter, for the window two ahead of the one it issues from.  Claims made at
+// the same time are neighbouring items, so the read window stays as narrow as
+// the static deal's, and a wave that runs fast claims more.  At the end every
+// wave holds at most two windows of claimed items.
+//
+// The ring itself (pieces, waits, asm loads, metadata, reduction) is
+// ring_sweep's; what changes is where a wave's k-th packet comes from:
+// s_claim[(k / 64) & 3][(k % 64) / G] holds its item, and the wave's packet
+// count grows as claims come back valid.  stamps (optional): t0/t1 per wave.
+template <int R, int G, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_window_dyn(const uint8_t* __restrict__ base,
+                                                         const lvlip_csum_desc* __restrict__ descs, uint32_t n,
+                                                         uint16_t* __restrict__ out, uint64_t* __restrict__ stamps) {
+    static_assert(G == 1 || G == 2 || G == 4, "groups tile a 64-packet window");
+    constexpr uint32_t GPW = 64u / G;  // groups per descriptor window
+    constexpr uint32_t END = 0xffffffffu;
+    constexpr uint32_t PIECE = 2048u;
+    constexpr uint32_t BAD = 0xffffffffu;
+    __shared__ uint4 s_win_all[WPB][2][64];
+    __shared__ uint32_t s_claim_all[WPB][4][GPW];
+    __shared__ uint32_t s_ctr;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lane16 = lane * 16u;
+    const uint32_t wid = uniform(threadIdx.x >> 6);
+    uint4(*s_win)[64] = s_win_all[wid];
+    uint32_t(*s_claim)[GPW] = s_claim_all[wid];
+    const uint64_t nw = (uint64_t)gridDim.x * WPB;
+    const uint64_t bx = (gridDim.x & 7u) == 0u ? (uint64_t)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                                               : (uint64_t)blockIdx.x;
+    const uint64_t ng = ((uint64_t)n + G - 1) / G;
+    // packet index of item `it`'s packet `p` (0 .. G-1), or BAD
+    auto item_pkt = [&](uint32_t it, uint32_t p) -> uint32_t {
+        if (it == BAD) return BAD;
+        const uint64_t g = (uint64_t)(it / WPB) * nw + bx * WPB + (it % WPB);
+        const uint64_t k = g * G + p;
+        return (g < ng && k < n) ? (uint32_t)k : BAD;
+    };
+    if (threadIdx.x == 0) s_ctr = 2u * GPW * WPB;
+    // static items of windows 0 and 1: j = v * GPW + q, r = wid
+    if (lane < 2u * GPW) s_claim[lane / GPW][lane % GPW] = lane * WPB + wid;
+    __syncthreads();
+
+    // packet of the wave's k (window v = k / 64 must have its claims in LDS)
+    auto wave_pkt = [&](uint32_t k) -> uint32_t {
+        return item_pkt(s_claim[(k >> 6) & 3u][(k & 63u) / G], k % G);
+    };
+    // cnt: the wave's packets known so far.  A window's claims are complete
+    // before it is fetched; valid packets are a prefix (items only grow).
+    uint32_t cnt = 0;
+    bool open = true;  // every packet so far valid: later windows may add more
+    auto extend = [&](uint32_t v) {  // window v's claims are in LDS
+        if (!open) return;
+        const uint32_t pk = wave_pkt(v * 64u + lane);
+        const uint64_t ok = __builtin_amdgcn_ballot_w64(pk != BAD);
+        const uint32_t c = (uint32_t)__builtin_popcountll(ok);
+        cnt = v * 64u + c;
+        open = c == 64u;
+    };
+    auto fetch = [&](uint32_t v) {  // descriptors of window v into s_win[v & 1]
+        uint32_t k = v * 64u + lane;
+        k = k < cnt ? k : (cnt ? cnt - 1u : 0u);
+        uint32_t pk = cnt ? wave_pkt(k) : 0u;
+        const lvlip_csum_desc* g = descs + pk;
+        uint4* win = s_win[v & 1u];
+        const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)win);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+        asm volatile("s_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                     :
+                     : "v"(g), "s"(lds)
+                     : "memory", "m0");
+#pragma clang diagnostic pop
+    };
+    extend(0);
+    extend(1);
+    if (cnt == 0) {
+        if (stamps && lane == 0) {
+            stamps[2 * (bx * WPB + wid)] = t_start;
+            stamps[2 * (bx * WPB + wid) + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+        return;
+    }
+    fetch(0);
+    fetch(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    uint32_t m_x, m_y, m_z, m_t, m_s;
+    auto load_window_meta = [&](uint32_t w) {
+        const uint4 d = s_win[w & 1u][lane];
+        const PacketMeta pm = packet_meta(base, u32x4{d.x, d.y, d.z, d.w});
+        m_x = pm.srd.x;
+        m_y = pm.srd.y;
+        m_z = pm.srd.z;
+        m_t = pm.tinfo;
+        m_s = pm.start;
+    };
+    load_window_meta(0);
+
+    uint32_t ip = 0, io = 0;
+    u32x4 srd;
+    uint32_t tinfo, start;
+    auto pull = [&](uint32_t k) {
+        srd.x = (uint32_t)__builtin_amdgcn_readlane((int)m_x, (int)k);
+        srd.y = (uint32_t)__builtin_amdgcn_readlane((int)m_y, (int)k);
+        srd.z = (uint32_t)__builtin_amdgcn_readlane((int)m_z, (int)k);
+        srd.w = SRD_WORD3;
+        tinfo = (uint32_t)__builtin_amdgcn_readlane((int)m_t, (int)k);
+        start = (uint32_t)__builtin_amdgcn_readlane((int)m_s, (int)k);
+    };
+    pull(0);
+    bool claiming = true;
+    // one claim per group, for the window two ahead of packet ip's
+    // (a slot not claimed is written BAD: the ring of four windows reuses slots)
+    auto claim = [&]() {
+        uint32_t it = BAD;
+        if (lane == 0) {
+            if (claiming) it = atomicAdd(&s_ctr, 1u);
+            s_claim[((ip >> 6) + 2u) & 3u][(ip & 63u) / G] = it;
+        }
+        it = (uint32_t)__builtin_amdgcn_readfirstlane((int)it);
+        if (item_pkt(it, 0) == BAD) claiming = false;  // every later item is past the pool
+    };
+    claim();  // group 0 of window 0 -> slot 0 of window 2
+
+    uint32_t gc = 0;
+    uint32_t res_w = 0, res_s = 0;
+    uint32_t acc = 0;
+    u32x4 va[R], vb[R];
+    uint32_t s_pkt[R], s_start[R], s_meta[R];
+
+    auto issue = [&](int r) {
+        const bool live = ip < cnt;
+        u32x4 sr = srd;
+        if (!live) sr.z = 0;
+        const uint32_t off = lane16 + io;
+        va[r] = buffer_load_nt_asm<0>(off, sr);
+        vb[r] = buffer_load_nt_asm<0>(off + 1024u, sr);
+        const bool last = io + PIECE >= srd.z;
+        s_pkt[r] = live ? ip : END;
+        s_start[r] = start;
+        s_meta[r] = (uint32_t)last | ((tinfo & 3u) << 1) | (((srd.z - 4u) - io) << 3);
+        if (live) {
+            if (!last) {
+                io += PIECE;
+            } else {
+                ++ip;
+                io = 0;
+                if (ip < cnt) {
+                    if ((ip & 63u) == 0u) {  // entered window ip/64
+                        lds_sync();          // lane 0's claims for window ip/64 + 1
+                        extend((ip >> 6) + 1u);
+                        load_window_meta(ip >> 6);
+                        fetch((ip >> 6) + 1u);
+                    }
+                    pull(ip & 63u);
+                    if (ip % G == 0u) claim();
+                }
+            }
+        }
+    };
+
+    auto consume = [&](int r) {
+        piece_wait<2 * (R - 1)>(va[r], vb[r]);
+        u32x4 x = va[r], y = vb[r];
+        const uint32_t meta = s_meta[r];
+        const uint32_t len3 = (meta >> 1) & 3u;
+        if ((meta & 1u) && len3) {
+            const uint32_t pos = meta >> 3;
+            const uint32_t m = (1u << (8u * len3)) - 1u;
+            const bool me = lane == ((pos >> 4) & 63u);
+            const uint32_t tk = (pos >> 2) & 3u;
+            const bool in_b = pos >= 1024u;
+            const uint32_t m0 = (me && tk == 0u) ? m : ~0u, m1 = (me && tk == 1u) ? m : ~0u;
+            const uint32_t m2 = (me && tk == 2u) ? m : ~0u, m3 = (me && tk == 3u) ? m : ~0u;
+            if (in_b) {
+                y.x &= m0; y.y &= m1; y.z &= m2; y.w &= m3;
+            } else {
+                x.x &= m0; x.y &= m1; x.z &= m2; x.w &= m3;
+            }
+        }
+        acc = dot2_acc(x.x, acc);
+        acc = dot2_acc(x.y, acc);
+        acc = dot2_acc(x.z, acc);
+        acc = dot2_acc(x.w, acc);
+        acc = dot2_acc(y.x, acc);
+        acc = dot2_acc(y.y, acc);
+        acc = dot2_acc(y.z, acc);
+        acc = dot2_acc(y.w, acc);
+        if (meta & 1u) {
+            const uint32_t w = wave_sum_dpp(acc);
+            acc = 0;
+            const uint32_t k = s_pkt[r] - gc;
+            if (lane == k) {
+                res_w = w;
+                res_s = s_start[r];
+            }
+            if (k == 63u || s_pkt[r] + 1u == cnt) {
+                uint32_t tt = res_s + res_w;
+                tt = (tt & 0xffffu) + (tt >> 16);
+                tt = (tt & 0xffffu) + (tt >> 16);
+                if (lane <= k) out[wave_pkt(gc + lane)] = (uint16_t)~tt;
+                gc += 64u;
+            }
+        }
+    };
+
+#pragma unroll
+    for (int r = 0; r < R; ++r) issue(r);
+    bool done = false;
+    while (!done) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (s_pkt[r] == END) {
+                done = true;
+                break;
+            }
+            consume(r);
+            issue(r);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (stamps && lane == 0) {
+        stamps[2 * (bx * WPB + wid)] = t_start;
+        stamps[2 * (bx * WPB + wid) + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // ------------------------------------ k_window with per-wave time stamps --
 //
 // Diagnostic (lvlip_lab_window_stamps): the product's k_window body, each wave
@@ -1404,6 +1643,14 @@ bool launch_wsflat(int u, int tile, int gord, int wgs_per_cu, hipStream_t s, con
     }
 }
 
+}  // namespace
+extern "C" __attribute__((visibility("default"))) int lvlip_lab_window_dyn(const void* base,
+                                                                        const lvlip_csum_desc* descs, uint32_t n,
+                                                                        uint16_t* out, uint64_t* stamps,
+                                                                        uint64_t stamp_bytes, int wpb, int shape,
+                                                                        void* stream);
+namespace {
+
 int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uint16_t* out, hipStream_t s,
                  const lvlip_launch_cfg* cfg) {
     const int kernel = cfg ? cfg->kernel : -1;
@@ -1612,6 +1859,17 @@ int lab_dispatch(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
             }
             break;
         }
+        case 15: {
+            // k_window_dyn: unroll = pieces in flight R (2) | packets per group G
+            // << 8 (1, 2, 4); waves_per_cu = waves per workgroup (8, 12), one
+            // workgroup per CU
+            int r = unroll & 0xff, g = (unroll >> 8) & 0xff;
+            if (r == 0) r = 2;
+            if (g == 0) g = 4;
+            const int w = wpc > 0 ? wpc : 12;
+            if (lvlip_lab_window_dyn(base, descs, n, out, nullptr, 0, w, r | (g << 8), s) < 0) return LVLIP_EINVAL;
+            break;
+        }
         case 5: {  // first-generation flat kernel
             const uint32_t grid = (uint32_t)(((uint64_t)n + lvlip::FLAT_T - 1) / lvlip::FLAT_T);
             hipLaunchKernelGGL(lvlip::k_flat, dim3(grid), dim3(lvlip::FLAT_T), 0, s, (const uint8_t*)base, descs,
@@ -1630,6 +1888,35 @@ extern "C" {
 // k_window R 2, G 4 (the MTU shape) at waves_per_cu waves on every CU, with
 // per-wave start/end stamps (2 u64 per wave) into `stamps`; returns the number
 // of waves (stamps needs 16 B each), or a negative LVLIP_E*.
+// k_window_dyn, one workgroup of wpb (8 or 12) waves per CU; shape = R | G << 8
+// (R 2; G 1, 2, 4); stamps (2 u64 per wave, XCD-major rank) or null.  Returns
+// the number of waves, or a negative LVLIP_E*.
+__attribute__((visibility("default"))) int lvlip_lab_window_dyn(const void* base, const lvlip_csum_desc* descs,
+                                                                uint32_t n, uint16_t* out, uint64_t* stamps,
+                                                                uint64_t stamp_bytes, int wpb, int shape,
+                                                                void* stream) {
+    if (n == 0) return LVLIP_OK;
+    if (!base || !descs || !out || n > LVLIP_MAX_BATCH || ((uintptr_t)base & 15u)) return LVLIP_EINVAL;
+    if (wpb != 8 && wpb != 12) return LVLIP_EINVAL;
+    const int r = shape & 0xff, g = (shape >> 8) & 0xff;
+    if (r != 2 || (g != 1 && g != 2 && g != 4)) return LVLIP_EINVAL;
+    uint64_t grid = (uint64_t)lvlip_host::current_cus();
+    const uint64_t ng = ((uint64_t)n + g - 1) / g;
+    // at least one group per wave's first window... keep grids with real work
+    while (grid > 8 && grid * wpb > ng) grid /= 2;
+    if (grid > 8) grid &= ~7ull;
+    if (stamps && grid * wpb * 16ull > stamp_bytes) return LVLIP_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+#define LVLIP_WDYN(GG, WW)                                                                          \
+    if (g == GG && wpb == WW) {                                                                     \
+        hipLaunchKernelGGL((lvlip::k_window_dyn<2, GG, WW>), dim3((uint32_t)grid), dim3(64 * WW), 0, s, \
+                           (const uint8_t*)base, descs, n, out, stamps);                           \
+    }
+    LVLIP_WDYN(1, 8) LVLIP_WDYN(2, 8) LVLIP_WDYN(4, 8) LVLIP_WDYN(1, 12) LVLIP_WDYN(2, 12) LVLIP_WDYN(4, 12)
+#undef LVLIP_WDYN
+    return hipGetLastError() == hipSuccess ? (int)(grid * wpb) : LVLIP_EHIP;
+}
+
 // wpb: waves per workgroup (4, 8 or 12): with wpb = waves_per_cu every CU runs
 // one workgroup.
 __attribute__((visibility("default"))) int lvlip_lab_window_stamps(const void* base, const lvlip_csum_desc* descs,

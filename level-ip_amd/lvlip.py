@@ -34,15 +34,15 @@ KERNEL_AUTO, KERNEL_FLAT, KERNEL_WINDOW, KERNEL_LANE = 0, 3, 8, 10
 # batch_dev sends these ids (and FLAT's A/B shapes) there, the product
 # returns EINVAL for them.  6 and 7 are retired round-1 ids (EINVAL everywhere).
 KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_WAVE_SIMPLE, KERNEL_FLAT_V1, KERNEL_WFLAT = 1, 2, 4, 5, 9
-KERNEL_RFLAT, KERNEL_WSFLAT, KERNEL_FLAT_OCC, KERNEL_FLAT_PERM = 11, 12, 13, 14
+KERNEL_RFLAT, KERNEL_WSFLAT, KERNEL_FLAT_OCC, KERNEL_FLAT_PERM, KERNEL_WINDOW_DYN = 11, 12, 13, 14, 15
 LAB_KERNELS = (KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_WAVE_SIMPLE, KERNEL_FLAT_V1, KERNEL_WFLAT, KERNEL_RFLAT,
-               KERNEL_WSFLAT, KERNEL_FLAT_OCC, KERNEL_FLAT_PERM)
+               KERNEL_WSFLAT, KERNEL_FLAT_OCC, KERNEL_FLAT_PERM, KERNEL_WINDOW_DYN)
 REG_DMA, REG_ZEROCOPY = 0, 1
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "wave_lds": KERNEL_WAVE_LDS,
                 "flat": KERNEL_FLAT, "wave_simple": KERNEL_WAVE_SIMPLE, "flat_v1": KERNEL_FLAT_V1,
                 "window": KERNEL_WINDOW, "wflat": KERNEL_WFLAT, "lane": KERNEL_LANE,
                 "rflat": KERNEL_RFLAT, "wsflat": KERNEL_WSFLAT, "flat_occ": KERNEL_FLAT_OCC,
-                "flat_perm": KERNEL_FLAT_PERM}
+                "flat_perm": KERNEL_FLAT_PERM, "window_dyn": KERNEL_WINDOW_DYN}
 KERNEL_LABELS = {v: k for k, v in KERNEL_NAMES.items()}
 
 # struct lvlip_csum_desc {u64 offset; i32 len; u32 start_sum;}  (16 B)

@@ -65,9 +65,19 @@ def main():
     nw = 0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
+    dyn = os.environ.get("TAIL_DYN") == "1"  # k_window_dyn (one workgroup of wpb waves per CU)
+    if dyn:
+        lab.lvlip_lab_window_dyn.restype = ctypes.c_int
+        lab.lvlip_lab_window_dyn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_void_p]
     for k in range(launches):
-        nw = lab.lvlip_lab_window_stamps(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
-                                         stamps[k].data_ptr(), nbytes, wpc, wpb, s.cuda_stream)
+        if dyn:
+            nw = lab.lvlip_lab_window_dyn(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
+                                          stamps[k].data_ptr(), nbytes, wpb, 2 | (4 << 8), s.cuda_stream)
+        else:
+            nw = lab.lvlip_lab_window_stamps(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
+                                             stamps[k].data_ptr(), nbytes, wpc, wpb, s.cuda_stream)
         assert nw > 0, nw
     e1.record(s)
     torch.cuda.synchronize()
@@ -110,7 +120,7 @@ def main():
     raw = st[2:5].tolist()
     summ["GBps_from_span"] = round(b.algo_bytes / (summ["span_us"] * 1e3), 1)
     summ["GBps_auto_events"] = round(b.algo_bytes / auto_ms / 1e6, 1)
-    rec = {"workload": wl, "waves_per_cu": wpc, "waves_per_workgroup": wpb, "waves": nw, "ms_per_launch_events": round(ms, 5),
+    rec = {"workload": wl, "waves_per_cu": wpc, "waves_per_workgroup": wpb, "dyn": dyn, "waves": nw, "ms_per_launch_events": round(ms, 5),
            "GBps": round(b.algo_bytes / ms / 1e6, 1), "median_over_launches_3_30": summ, "launches": res,
            "raw_stamps_launches_3_5": raw}
     print(json.dumps({k2: rec[k2] for k2 in ("workload", "waves", "ms_per_launch_events", "GBps")}), summ,

@@ -77,6 +77,9 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT_OCC, 0x4508 | (4 << 16), 0),  # + last round dealt to all four waves
     (lvlip.KERNEL_FLAT_OCC, 0x4508 | (8 << 16), 0),  # + no early exit from a round
     (lvlip.KERNEL_FLAT_PERM, 16 | (2 << 8) | (1 << 12), 0),  # run-dealt tile map (identity below a generation)
+    (lvlip.KERNEL_WINDOW_DYN, 2 | (4 << 8), 12),  # window deal, items claimed in the CU's workgroup
+    (lvlip.KERNEL_WINDOW_DYN, 2 | (1 << 8), 8),
+    (lvlip.KERNEL_WINDOW_DYN, 2 | (2 << 8), 12),
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
@@ -264,7 +267,8 @@ def test_full_size_bit_exact(name):
                     (lvlip.KERNEL_FLAT_PERM, 16 | (2 << 8) | (1 << 12), 0),
                     (lvlip.KERNEL_FLAT_PERM, 16 | (2 << 8), 0),
                     (lvlip.KERNEL_FLAT_PERM, 32 | (1 << 8) | (1 << 12), 0),
-                    (lvlip.KERNEL_FLAT_PERM, 64 | (2 << 8) | (1 << 12), 0)]:
+                    (lvlip.KERNEL_FLAT_PERM, 64 | (2 << 8) | (1 << 12), 0),
+                    (lvlip.KERNEL_WINDOW_DYN, 2 | (4 << 8), 12), (lvlip.KERNEL_WINDOW_DYN, 2 | (2 << 8), 8)]:
         assert np.array_equal(run(base, descs, variant, out), want), variant
     # adversarial packets really are there and fold as the reference does
     ones = b.paint == 2

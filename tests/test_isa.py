@@ -80,7 +80,7 @@ def stream_kernels(asm):
 
 def pieces(name):
     """R (pieces in flight) of a k_stream / k_window instantiation."""
-    return int(re.search(r"k_(?:stream|window|window_stamp)ILi(\d+)E", name).group(1))
+    return int(re.search(r"k_(?:stream|window|window_stamp|window_dyn)ILi(\d+)E", name).group(1))
 
 
 def test_buffer_loads_padded_against_valu_sgpr_hazard(asm):
