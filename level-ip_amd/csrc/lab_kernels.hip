@@ -1244,8 +1244,9 @@ __global__ __launch_bounds__(64 * WPB) void k_window_dyn(const uint8_t* __restri
         return (g < ng && k < n) ? (uint32_t)k : BAD;
     };
     if (threadIdx.x == 0) s_ctr = 2u * GPW * WPB;
-    // static items of windows 0 and 1: j = v * GPW + q, r = wid
-    if (lane < 2u * GPW) s_claim[lane / GPW][lane % GPW] = lane * WPB + wid;
+    // static items of windows 0 and 1: j = v * GPW + q, r = wid (2 GPW slots:
+    // 128 for G = 1, so two passes of the wave's lanes)
+    for (uint32_t q = lane; q < 2u * GPW; q += 64u) s_claim[q / GPW][q % GPW] = q * WPB + wid;
     __syncthreads();
 
     // packet of the wave's k (window v = k / 64 must have its claims in LDS)
@@ -1259,8 +1260,9 @@ __global__ __launch_bounds__(64 * WPB) void k_window_dyn(const uint8_t* __restri
     auto extend = [&](uint32_t v) {  // window v's claims are in LDS
         if (!open) return;
         const uint32_t pk = wave_pkt(v * 64u + lane);
+        // valid packets are a prefix of the window: count the leading ones
         const uint64_t ok = __builtin_amdgcn_ballot_w64(pk != BAD);
-        const uint32_t c = (uint32_t)__builtin_popcountll(ok);
+        const uint32_t c = ~ok == 0ull ? 64u : (uint32_t)__builtin_ctzll(~ok);
         cnt = v * 64u + c;
         open = c == 64u;
     };
@@ -1268,6 +1270,7 @@ __global__ __launch_bounds__(64 * WPB) void k_window_dyn(const uint8_t* __restri
         uint32_t k = v * 64u + lane;
         k = k < cnt ? k : (cnt ? cnt - 1u : 0u);
         uint32_t pk = cnt ? wave_pkt(k) : 0u;
+        pk = pk == BAD ? 0u : pk;  // (never: k < cnt; keeps the DMA inside the array)
         const lvlip_csum_desc* g = descs + pk;
         uint4* win = s_win[v & 1u];
         const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane(
@@ -1407,7 +1410,8 @@ __global__ __launch_bounds__(64 * WPB) void k_window_dyn(const uint8_t* __restri
                 uint32_t tt = res_s + res_w;
                 tt = (tt & 0xffffu) + (tt >> 16);
                 tt = (tt & 0xffffu) + (tt >> 16);
-                if (lane <= k) out[wave_pkt(gc + lane)] = (uint16_t)~tt;
+                const uint32_t pk = lane <= k ? wave_pkt(gc + lane) : BAD;
+                if (pk != BAD) out[pk] = (uint16_t)~tt;
                 gc += 64u;
             }
         }
