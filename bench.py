@@ -670,8 +670,9 @@ def frames_dev(lvlip, torch, dev):
     res = {}
     for name, fn, nbytes in (
             ("tx_fill", lambda: lvlip.tx_checksum_dev(base, fdt, stream=stream), 20 * n + l4_bytes),
-            # A/B (liblvlip_lab.so): the same with plain (temporal) field stores
-            ("tx_fill_plain", lambda: lvlip.frames_variant_dev(0, 1, base, fdt, stream=stream),
+            # A/B (liblvlip_lab.so): the same shape (U 8, blocks) with plain
+            # (temporal) field stores
+            ("tx_fill_plain", lambda: lvlip.frames_variant_dev(0, 1 | 2 | 4, base, fdt, stream=stream),
              20 * n + l4_bytes),
             ("rx_header", lambda: lvlip.rx_verify_dev(base, fdt, 0, stream=stream), 20 * n),
             # A/B: the header call on k_flat2 with a frame source

@@ -583,8 +583,10 @@ int lvlip_rx_verify_dev(const void* base, const lvlip_frame_desc* frames, uint32
     if (n == 0) return LVLIP_OK;
     if (!base || !frames || !verdict || n > kMaxFrames || ((uintptr_t)base & 15u)) return LVLIP_EINVAL;
     hipStream_t s = (hipStream_t)stream;
+    // RX + L4: U 4 in block order (round 3, same process: 253 vs 257 us for
+    // quarters on 2M frames, U 8 258-259; profiles/r03_ab_frames_shape.json)
     const int rc = (flags & LVLIP_RX_VERIFY_L4)
-                       ? lvlip::launch_frames_flat<lvlip::FR_RX_L4, 4, 1>(base, frames, n, verdict, s, true)
+                       ? lvlip::launch_frames_flat<lvlip::FR_RX_L4, 4, 2>(base, frames, n, verdict, s, true)
                        : launch_rx_hdr(base, frames, n, verdict, s);
     if (rc == LVLIP_EHIP) return hip_fail(hipGetLastError(), "frame call");
     return rc;
@@ -594,7 +596,9 @@ int lvlip_tx_checksum_dev(void* base, const lvlip_frame_desc* frames, uint32_t n
                           void* /*workspace*/, void* stream) {
     if (n == 0) return LVLIP_OK;
     if (!base || !frames || n > kMaxFrames || ((uintptr_t)base & 15u)) return LVLIP_EINVAL;
-    const int rc = lvlip::launch_frames_flat<lvlip::FR_TX, 4, 1>(base, frames, n, status, (hipStream_t)stream,
+    // U 8 in block order (round 3, same process: 369 vs 374 us for U 4
+    // quarters on 2M frames; profiles/r03_ab_frames_shape.json)
+    const int rc = lvlip::launch_frames_flat<lvlip::FR_TX, 8, 2>(base, frames, n, status, (hipStream_t)stream,
                                                                 true);
     if (rc == LVLIP_EHIP) return hip_fail(hipGetLastError(), "frame call");
     return rc;
