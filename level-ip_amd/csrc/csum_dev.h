@@ -613,7 +613,7 @@ __device__ __forceinline__ uint32_t byte_range_mask(int b0, int b1, int j) {
 // and big-packet slots follow from one exclusive scan of its D counts.
 // FIN_LDS (A/B, lab): phase 4's per-descriptor words go through LDS instead of
 // staying in registers across the sweep (fewer VGPRs live in phase 2).
-// PFA (DescSrc only; the product's batch calls use kFlatPrefetchTiles): each
+// PFA (the product's batch calls use kFlatPrefetchTiles; frame sources A/B): each
 // thread also loads the descriptor PFA tiles ahead of its own, issued after
 // its own (loads return in order, so its own descriptor's wait does not cover
 // it).  Block b runs on XCD b % 8 (as observed), so with PFA a multiple of 8
@@ -1185,7 +1185,7 @@ namespace lvlip {
 // frame source (flat_src.h) per at most kLaunchMax entries, whole frames per
 // launch.  Returns LVLIP_EHIP when a launch fails (the error stays readable by
 // hipGetLastError).
-template <int MODE, int U, int GORD>
+template <int MODE, int U, int GORD, int PFA = 0>
 int launch_frames_flat(const void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* out8,
                        hipStream_t s, bool nt_store) {
     using Src = FrameSrc<MODE>;
@@ -1196,8 +1196,8 @@ int launch_frames_flat(const void* base, const lvlip_frame_desc* frames, uint32_
         const uint32_t grid = (uint32_t)(((uint64_t)entries + FT - 1) / FT);
         Src src{(const uint8_t*)base, (uint8_t*)base, frames + f0, out8 ? out8 + f0 : nullptr};
         src.nt_store = nt_store;
-        hipLaunchKernelGGL((k_flat2<U, true, GORD, Src>), dim3(grid), dim3(FT), 0, s, (const uint8_t*)base,
-                           src, entries);
+        hipLaunchKernelGGL((k_flat2<U, true, GORD, Src, 1, false, PFA>), dim3(grid), dim3(FT), 0, s,
+                           (const uint8_t*)base, src, entries);
         if (hipPeekAtLastError() != hipSuccess) return LVLIP_EHIP;
         f0 += m;
     }

@@ -173,6 +173,9 @@ struct FrameSrc {
     uint8_t* out8;                   // RX: verdict[], TX: status[] (may be null)
     bool nt_store = false;           // TX: nontemporal field stores (the launcher's default)
     static constexpr uint32_t SLOTS = MODE == FR_RX ? 1u : 2u;
+    // the frame descriptor of entry i (k_flat2's PFA prefetch: 16 B, like a
+    // batch descriptor)
+    __device__ __forceinline__ const lvlip_frame_desc* desc_ptr(uint32_t i) const { return frames + i / SLOTS; }
     // The parse window's chunks are in registers after get(): k_flat2 sums
     // each entry's bytes inside the window there and sweeps only the rest, so
     // no frame byte is read from HBM twice.

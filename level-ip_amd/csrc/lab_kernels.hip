@@ -1972,7 +1972,8 @@ __attribute__((visibility("default"))) int lvlip_lab_batch_dev_ex(const void* ba
 // mode: 0 TX fill, 1 RX header (the flat sweep instead of k_rx_hdr), 2 RX +
 // L4; 3 the header-only call on k_rx_hdr with a descriptor prefetch.  variant
 // bits (modes 0-2): 1 plain (temporal) TX field stores, 2 eight loads per
-// round, 4 block group order (else quarters); mode 3: the prefetch distance
+// round, 4 block group order (else quarters), 8 block order with the frame
+// descriptors prefetched 1 280 tiles ahead (k_flat2's PFA); mode 3: the prefetch distance
 // (variant >> 3) x 160 blocks.
 __attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int variant, void* base,
                                                                 const lvlip_frame_desc* frames, uint32_t n,
@@ -1981,12 +1982,14 @@ __attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int va
     if (!base || !frames || n > LVLIP_MAX_BATCH / 2u || ((uintptr_t)base & 15u)) return LVLIP_EINVAL;
     if (mode != 0 && !out8) return LVLIP_EINVAL;
     hipStream_t s = (hipStream_t)stream;
-    const bool nt = !(variant & 1), u8 = variant & 2, blocks = variant & 4;
+    const bool nt = !(variant & 1), u8 = variant & 2, blocks = variant & 4, pf = (variant & 8) && mode != 3;
 #define LVLIP_LAB_FR(M)                                                                              \
-    (u8 ? (blocks ? lvlip::launch_frames_flat<M, 8, 2>(base, frames, n, out8, s, nt)                \
-                  : lvlip::launch_frames_flat<M, 8, 1>(base, frames, n, out8, s, nt))               \
-        : (blocks ? lvlip::launch_frames_flat<M, 4, 2>(base, frames, n, out8, s, nt)                \
-                  : lvlip::launch_frames_flat<M, 4, 1>(base, frames, n, out8, s, nt)))
+    (pf ? (u8 ? lvlip::launch_frames_flat<M, 8, 2, 1280>(base, frames, n, out8, s, nt)              \
+              : lvlip::launch_frames_flat<M, 4, 2, 1280>(base, frames, n, out8, s, nt))             \
+        : u8 ? (blocks ? lvlip::launch_frames_flat<M, 8, 2>(base, frames, n, out8, s, nt)           \
+                       : lvlip::launch_frames_flat<M, 8, 1>(base, frames, n, out8, s, nt))          \
+             : (blocks ? lvlip::launch_frames_flat<M, 4, 2>(base, frames, n, out8, s, nt)           \
+                       : lvlip::launch_frames_flat<M, 4, 1>(base, frames, n, out8, s, nt)))
     switch (mode) {
         case 0: return LVLIP_LAB_FR(lvlip::FR_TX);
         case 1: return LVLIP_LAB_FR(lvlip::FR_RX);

@@ -65,7 +65,8 @@ def main():
         "tx_product": lambda: lvlip.tx_checksum_dev(base, fdt, stream=s),
         "rx_l4_product": lambda: lvlip.rx_verify_dev(base, fdt, lvlip.RX_VERIFY_L4, stream=s),
     }
-    for v, name in ((0, "u4_quarters"), (2, "u8_quarters"), (4, "u4_blocks"), (6, "u8_blocks")):
+    for v, name in ((0, "u4_quarters"), (2, "u8_quarters"), (4, "u4_blocks"), (6, "u8_blocks"),
+                    (12, "u4_blocks_pf"), (14, "u8_blocks_pf")):
         calls[f"tx_{name}"] = (lambda vv: lambda: lvlip.frames_variant_dev(0, vv, base, fdt, stream=s))(v)
         calls[f"rx_l4_{name}"] = (lambda vv: lambda: lvlip.frames_variant_dev(2, vv, base, fdt, stream=s))(v)
 
