@@ -77,8 +77,7 @@ def parse(argv=None):
                    help="packets (frames for mixed) per rank (--packets under torch.distributed.run, "
                         "whose own parser takes --n for a prefix of its options)")
     p.add_argument("--kernel", default="auto",
-                   choices=["auto", "wave", "wave_lds", "flat", "wave_simple", "flat_v1", "window", "wflat",
-                            "lane"])
+                   choices=["auto", "wave", "flat", "window", "wflat", "lane"])
     p.add_argument("--unroll", type=int, default=0)
     p.add_argument("--waves-per-cu", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -625,8 +624,7 @@ def sweep(lvlip, torch, base, descs, out, b, stream):
     res = {}
     variants = [("window", 2 | (4 << 8), 16), ("window", 2 | (4 << 8), 12), ("window", 2 | (2 << 8), 8),
                 ("window", 2 | (3 << 8), 8), ("wave", 2, 8), ("wave", 2, 12), ("wave", 3, 12),
-                ("wave_simple", 2, 0), ("wave_lds", 2, 0), ("flat", 4, 0), ("flat", 8, 0),
-                ("flat", 8 | (2 << 8), 0), ("wflat", 0, 0), ("flat_v1", 0, 0)]
+                ("flat", 4, 0), ("flat", 8, 0), ("flat", 8 | (2 << 8), 0), ("wflat", 0, 0)]
     for rnd in range(2):  # interleaved rounds in one process
         for k, u, w in variants:
             def f():

@@ -19,6 +19,9 @@
  *  Group 3 — host-resident batches through a per-thread context (pinned
  *    staging arena + HIP stream): gathers skb bytes, H2D, kernel, D2H.
  *
+ *  Group 4 — one batch over several GPUs: a byte-balanced contiguous
+ *    partition, and a host batch run by one thread per device context.
+ *
  * Error convention: 0 = success, negative LVLIP_E* on failure.  A batch call
  * that fails writes nothing meaningful to out[] and never substitutes a CPU
  * result: the caller decides what to do.
@@ -36,7 +39,13 @@ extern "C" {
  * declared in this header are exported. */
 #pragma GCC visibility push(default)
 
-#define LVLIP_CSUM_ABI_VERSION 1
+/* 2 (round 4): ids 1, 2, 4, 6, 7 and 9 are no longer accepted by
+ * lvlip_csum_batch_dev_ex (LVLIP_EINVAL: A/B variants, liblvlip_lab.so), and
+ * FLAT's unroll takes only 2, 4 or 8 (the group-order bits << 8 and the
+ * 512-descriptor tile bit 1 << 10 are refused); added Group 4
+ * (lvlip_partition_bytes, lvlip_csum_batch_host_flat_multi) and
+ * lvlip_icmp_echo_reply_dev_ex (include/lvlip_skb.h).  INTEGRATION.md §5. */
+#define LVLIP_CSUM_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------- */
 #define LVLIP_OK              0
@@ -223,6 +232,35 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx *ctx, const void *base,
 #define LVLIP_REG_ZEROCOPY 1u
 int lvlip_csum_register(lvlip_csum_ctx *ctx, void *ptr, size_t bytes, uint32_t flags);
 int lvlip_csum_unregister(lvlip_csum_ctx *ctx, void *ptr);
+
+/* ======================================================================= */
+/* Group 4: one batch over several GPUs                     */
+/* ======================================================================= */
+
+/* Packets are independent, so a batch shards by contiguous descriptor ranges
+ * with no exchange on the data path.  Fills cuts[0 .. parts] (parts + 1
+ * entries): part p is descriptors [cuts[p], cuts[p + 1]), cuts[0] = 0,
+ * cuts[parts] = n, non-decreasing.  Balanced by bytes: part p takes the
+ * descriptors whose byte prefix (sum of max(len, 0) before them) lies in
+ * [p T / parts, (p + 1) T / parts), T the total, so a ragged batch gives
+ * every GPU about the same HBM traffic; an all-empty batch splits by count.
+ * The same cuts as level-ip_amd/shard.py partition().  Host only (no GPU).
+ * Returns 0, or LVLIP_EINVAL (parts == 0, NULL with n > 0). */
+int lvlip_partition_bytes(const lvlip_csum_desc *d, uint32_t n, uint32_t parts,
+                          uint32_t *cuts);
+
+/* lvlip_csum_batch_host_flat over nctx contexts at once (one per GPU, each
+ * created with lvlip_csum_ctx_create on its own device): the batch is cut
+ * with lvlip_partition_bytes into nctx parts, and context k checksums part k
+ * on a host thread of its own (its gather, copies and kernel overlap with the
+ * other devices').  Waits for all parts; out[] is in descriptor order.  The
+ * contexts are used by this call's threads only while it runs (the caller
+ * must not use them concurrently).  Returns 0 or the first part's LVLIP_E*
+ * in part order (results of failed parts are not meaningful). */
+int lvlip_csum_batch_host_flat_multi(lvlip_csum_ctx *const *ctxs, uint32_t nctx,
+                                     const void *base, size_t base_bytes,
+                                     const lvlip_csum_desc *d, uint32_t n,
+                                     uint16_t *out);
 
 /* ======================================================================= */
 /* Misc                                                                     */

@@ -170,14 +170,35 @@ int lvlip_tx_checksum_dev(void *base, const lvlip_frame_desc *frames, uint32_t n
 
 /* f4 on frames in HBM: lvlip_icmp_echo_reply_fill in one launch, one lane per
  * frame.  Every frame that is an IPv4 ICMP echo request (type 8, code 0, the
- * message inside the frame) whose ICMP checksum verified becomes the reply's
- * ICMP part: type 0 and the RFC 1624 checksum field, bit-identical to
- * icmpv4_reply's full recomputation (src/icmpv4.c:44-47); in the one
+ * message inside the frame) becomes the reply's ICMP part: type 0 and the
+ * RFC 1624 checksum field derived from the request's field alone; in the one
  * undecidable case (LVLIP_CSUM_RECOMPUTE) the lane sums the message itself.
  * status[i] (may be NULL): 1 updated from the field, 2 recomputed, 0 not an
- * echo request (frame untouched).  Nothing else of the message is read. */
+ * echo request (frame untouched).  Nothing else of the message is read.
+ *
+ * PRECONDITION: the request's ICMP checksum verified (e.g. the frame got
+ * LVLIP_RX_OK from lvlip_rx_verify_dev with LVLIP_RX_VERIFY_L4).  Only then
+ * is the field bit-identical to icmpv4_reply's full recomputation
+ * (src/icmpv4.c:44-47).  The call does NOT check it: status 1 does not mean
+ * the request verified, and for a request whose checksum is wrong the field
+ * written differs from the reference's (which answers such requests with a
+ * correct checksum, src/icmpv4.c:11 never verifies).  For frames nobody
+ * verified, use lvlip_icmp_echo_reply_dev_ex with LVLIP_ECHO_FULL. */
 int lvlip_icmp_echo_reply_dev(void *base, const lvlip_frame_desc *frames, uint32_t n,
                               uint8_t *status, void *stream);
+
+/* flags of lvlip_icmp_echo_reply_dev_ex */
+#define LVLIP_ECHO_FULL 0x1u /* sum every request's message (one lane per frame)
+                                and write icmpv4_reply's field exactly: for
+                                any request, verified or not; status 2 */
+
+/* lvlip_icmp_echo_reply_dev with flags: 0 is lvlip_icmp_echo_reply_dev (the
+ * precondition above holds); LVLIP_ECHO_FULL computes the reply's field as
+ * icmpv4_reply does, from the whole message with type and field zeroed
+ * (src/icmpv4.c:45-47), bit-identical for every echo request.  Other flag bits
+ * are LVLIP_EINVAL. */
+int lvlip_icmp_echo_reply_dev_ex(void *base, const lvlip_frame_desc *frames, uint32_t n,
+                                 uint32_t flags, uint8_t *status, void *stream);
 
 /* RFC 1071 pseudo-header seed with the carries folded back (for RX verify of
  * checksums produced by RFC-correct peers). */

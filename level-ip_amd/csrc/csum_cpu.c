@@ -229,3 +229,37 @@ void ip_send_check(struct iphdr *ihdr)
     const uint16_t c = checksum(h, (h[0] & 0x0f) * 4, 0);
     memcpy(h + 10, &c, 2);
 }
+
+/* Group 4 (include/lvlip_csum.h): contiguous, byte-balanced cuts, the same as
+ * level-ip_amd/shard.py partition(): cut p is the first index whose byte
+ * prefix reaches p * T / parts (numpy searchsorted, side "left").  One pass:
+ * the targets increase with p.  The products are 128-bit (T < 2^63). */
+int lvlip_partition_bytes(const lvlip_csum_desc *d, uint32_t n, uint32_t parts, uint32_t *cuts)
+{
+    if (parts == 0 || !cuts || (n && !d))
+        return LVLIP_EINVAL;
+    cuts[0] = 0;
+    for (uint32_t p = 1; p <= parts; ++p)
+        cuts[p] = n;
+    if (parts == 1 || n == 0)
+        return LVLIP_OK;
+    unsigned __int128 total = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        total += d[i].len > 0 ? (uint32_t)d[i].len : 0u;
+    if (total == 0) {
+        for (uint32_t p = 1; p < parts; ++p)
+            cuts[p] = (uint32_t)((uint64_t)n * p / parts);
+        return LVLIP_OK;
+    }
+    uint32_t i = 0;
+    unsigned __int128 pre = 0; /* bytes of descriptors [0, i) */
+    for (uint32_t p = 1; p < parts; ++p) {
+        const unsigned __int128 target = total * p / parts;
+        while (i < n && pre < target) {
+            pre += d[i].len > 0 ? (uint32_t)d[i].len : 0u;
+            ++i;
+        }
+        cuts[p] = i;
+    }
+    return LVLIP_OK;
+}

@@ -491,4 +491,36 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
     return finish_pieces(c, rc);
 }
 
+// Group 4: one host thread per context, each on its part of the batch.  The
+// parts' descriptors keep their offsets from `base`, so each context gathers
+// (or DMAs) only its own span.
+int lvlip_csum_batch_host_flat_multi(lvlip_csum_ctx* const* ctxs, uint32_t nctx, const void* base,
+                                     size_t base_bytes, const lvlip_csum_desc* d, uint32_t n, uint16_t* out) {
+    if (!ctxs || nctx == 0 || (n && (!base || !d || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
+    for (uint32_t k = 0; k < nctx; ++k)
+        if (!ctxs[k]) return LVLIP_EINVAL;
+    if (n == 0) return LVLIP_OK;
+    std::vector<uint32_t> cuts(nctx + 1u);
+    int rc = lvlip_partition_bytes(d, n, nctx, cuts.data());
+    if (rc != LVLIP_OK) return rc;
+    std::vector<int> rcs(nctx, LVLIP_OK);
+    auto part = [&](uint32_t k) {
+        const uint32_t lo = cuts[k], hi = cuts[k + 1];
+        if (hi > lo) rcs[k] = lvlip_csum_batch_host_flat(ctxs[k], base, base_bytes, d + lo, hi - lo, out + lo);
+    };
+    std::vector<std::thread> th;
+    th.reserve(nctx);
+    try {
+        for (uint32_t k = 1; k < nctx; ++k) th.emplace_back(part, k);
+    } catch (...) {
+        rc = LVLIP_ENOMEM;  // no thread: the parts already started still finish below
+    }
+    part(0);  // part 0 on the calling thread
+    for (auto& t : th) t.join();
+    if (rc != LVLIP_OK) return rc;
+    for (uint32_t k = 0; k < nctx; ++k)
+        if (rcs[k] != LVLIP_OK) return rcs[k];
+    return LVLIP_OK;
+}
+
 }  // extern "C"

@@ -17,8 +17,8 @@
 //               scan.  Also the frame calls' kernel (flat_src.h).
 //   k_lane    : up to 32 B (IPv4 headers alone): a few lanes per packet.
 //   k_rx_hdr  : the header-only RX frame call, one lane per frame (csum_dev.h).
-//   k_echo_reply : f4, the RFC 1624 echo reply of verified requests, one lane
-//               per frame.
+//   k_echo_reply : f4, the RFC 1624 echo reply of verified requests (or, with
+//               LVLIP_ECHO_FULL, icmpv4_reply's full sum), one lane per frame.
 // The A/B variants measured against these (k_stream, k_wflat, k_rflat,
 // k_wsflat, the round-1 kernels, k_flat2's other shapes) live in
 // liblvlip_lab.so (lab_kernels.hip).
@@ -186,6 +186,29 @@ __device__ __forceinline__ uint32_t oc_add16(uint32_t a, uint32_t b) {
     return (t & 0xffffu) + (t >> 16);
 }
 
+// FULL (LVLIP_ECHO_FULL): the lane sums the whole request message W (16-B
+// aligned chunk loads, bytes outside it masked) and writes icmpv4_reply's own
+// result, finish(0, W - 0x0008 - HC): the reply's message is the request's
+// with word 0 (type 8, code 0 = LE word 0x0008) and word 1 (the field)
+// zeroed, and u32 sums differ by exactly those words.  No precondition.
+__device__ __forceinline__ uint32_t msg_word_sum(const uint8_t* m, uint32_t len) {
+    const uint64_t a = reinterpret_cast<uint64_t>(m);
+    const uint64_t a0 = a & ~15ull;
+    const uint32_t lo = (uint32_t)(a & 15ull);
+    const uint32_t span = lo + len;
+    const uint32_t nch = (span + 15u) >> 4;
+    const uint32_t lastv = span - 16u * (nch - 1u);
+    const bool odd = a & 1ull;
+    uint32_t acc = 0;
+    for (uint32_t c = 0; c < nch; ++c) {
+        uint4 v = load_global(a0 + 16ull * c);
+        v = mask_chunk(v, c == 0u ? (int)lo : 0, c + 1u == nch ? (int)lastv : 16);
+        acc += odd ? chunk_words<true>(v) : chunk_words<false>(v);
+    }
+    return acc;
+}
+
+template <bool FULL>
 __global__ __launch_bounds__(256) void k_echo_reply(uint8_t* __restrict__ base,
                                                     const lvlip_frame_desc* __restrict__ frames,
                                                     uint32_t n, uint8_t* __restrict__ status) {
@@ -223,7 +246,10 @@ __global__ __launch_bounds__(256) void k_echo_reply(uint8_t* __restrict__ base,
                 const uint32_t S = hc == 0xffffu ? 0xffffu : (~hc & 0xffffu);
                 const uint32_t S1 = oc_add16(S, 0xffffu - 0x0008u);
                 uint32_t field;
-                if (S1 != 0xffffu) {
+                if (FULL) {
+                    field = finish(0u, msg_word_sum(h + l4, icmp_len) - 0x0008u - hc);
+                    st = 2u;
+                } else if (S1 != 0xffffu) {
                     field = ~S1 & 0xffffu;
                     st = 1u;
                 } else {
@@ -488,7 +514,7 @@ static uint32_t launch_piece(const lvlip_launch_cfg& c, uint32_t n) {
     // a launch, and the window of the batch they read widens.  A batch of more
     // than 1.5 x kWindowGroupsPerWave groups per wave goes out as launches of
     // about kWindowGroupsPerWave groups per wave, back to back on the stream,
-    // which restart the waves in step (scripts/split_tune_once.sh:
+    // which restart the waves in step (round 3's split_tune_once.sh:
     // 8M MTU segments 6 725 GB/s in one launch, 6 866 in 8; 64M 6 450 in one,
     // 6 850 in 64; 1M jumbo 7 113 in one, 7 146 in 2).  The configs' 1M MTU
     // batch (85 groups per wave) stays one launch.  Results are the same bits:
@@ -585,9 +611,10 @@ int lvlip_rx_verify_dev(const void* base, const lvlip_frame_desc* frames, uint32
     hipStream_t s = (hipStream_t)stream;
     // RX + L4: U 4 in block order (round 3, same process: 253 vs 257 us for
     // quarters on 2M frames, U 8 258-259; profiles/r03_ab_frames_shape.json)
-    const int rc = (flags & LVLIP_RX_VERIFY_L4)
-                       ? lvlip::launch_frames_flat<lvlip::FR_RX_L4, 4, 2>(base, frames, n, verdict, s, true)
-                       : launch_rx_hdr(base, frames, n, verdict, s);
+    // launch_rx_hdr records its own HIP error (hip_fail clears it with
+    // hipGetLastError); launch_frames_flat leaves it pending (hipPeekAtLastError)
+    if (!(flags & LVLIP_RX_VERIFY_L4)) return launch_rx_hdr(base, frames, n, verdict, s);
+    const int rc = lvlip::launch_frames_flat<lvlip::FR_RX_L4, 4, 2>(base, frames, n, verdict, s, true);
     if (rc == LVLIP_EHIP) return hip_fail(hipGetLastError(), "frame call");
     return rc;
 }
@@ -597,27 +624,40 @@ int lvlip_tx_checksum_dev(void* base, const lvlip_frame_desc* frames, uint32_t n
     if (n == 0) return LVLIP_OK;
     if (!base || !frames || n > kMaxFrames || ((uintptr_t)base & 15u)) return LVLIP_EINVAL;
     // U 8 in block order (round 3, same process: 369 vs 374 us for U 4
-    // quarters on 2M frames; profiles/r03_ab_frames_shape.json)
-    const int rc = lvlip::launch_frames_flat<lvlip::FR_TX, 8, 2>(base, frames, n, status, (hipStream_t)stream,
-                                                                true);
+    // quarters on 2M frames; profiles/r03_ab_frames_shape.json); the field
+    // stores `nt sc0 sc1` (round 4, same process, 7 rounds on 2M frames:
+    // 364.1 vs 369.6 us for nt, 392.7 plain, 385 sc1, 420 / 410 whole 32-B /
+    // 64-B blocks; profiles/r04_tx_store.json)
+    const int rc = lvlip::launch_frames_flat<lvlip::FR_TX, 8, 2, 0, 0, 6>(base, frames, n, status,
+                                                                         (hipStream_t)stream, true);
     if (rc == LVLIP_EHIP) return hip_fail(hipGetLastError(), "frame call");
     return rc;
 }
 
-int lvlip_icmp_echo_reply_dev(void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* status,
-                              void* stream) {
+int lvlip_icmp_echo_reply_dev_ex(void* base, const lvlip_frame_desc* frames, uint32_t n, uint32_t flags,
+                                 uint8_t* status, void* stream) {
+    if (flags & ~LVLIP_ECHO_FULL) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
     if (!base || !frames || ((uintptr_t)base & 15u)) return LVLIP_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     for (uint32_t f0 = 0; f0 < n;) {
         const uint32_t m = n - f0 < kLaunchMax ? n - f0 : kLaunchMax;
-        hipLaunchKernelGGL(lvlip::k_echo_reply, dim3((m + 255u) / 256u), dim3(256), 0, s, (uint8_t*)base,
-                           frames + f0, m, status ? status + f0 : nullptr);
+        if (flags & LVLIP_ECHO_FULL)
+            hipLaunchKernelGGL(lvlip::k_echo_reply<true>, dim3((m + 255u) / 256u), dim3(256), 0, s, (uint8_t*)base,
+                               frames + f0, m, status ? status + f0 : nullptr);
+        else
+            hipLaunchKernelGGL(lvlip::k_echo_reply<false>, dim3((m + 255u) / 256u), dim3(256), 0, s,
+                               (uint8_t*)base, frames + f0, m, status ? status + f0 : nullptr);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "k_echo_reply");
         f0 += m;
     }
     return LVLIP_OK;
+}
+
+int lvlip_icmp_echo_reply_dev(void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* status,
+                              void* stream) {
+    return lvlip_icmp_echo_reply_dev_ex(base, frames, n, 0u, status, stream);
 }
 
 }  // extern "C"

@@ -159,14 +159,95 @@ struct FrWin {
     __device__ __forceinline__ uint32_t le32(uint32_t o) const { return le16(o) | (le16(o + 2u) << 16); }
 };
 
+// TX plan-word bits of the whole-sector field stores (FrameSrc<FR_TX, SEC>,
+// SEC > 0): the aligned SEC-byte block around the header / L4 checksum field
+// lies wholly inside the frame; both fields share one block.  Bits 24-31 hold
+// the L4 field's distance from the header field.
+constexpr uint32_t FR_SEC_HDR = 0x2;
+constexpr uint32_t FR_SEC_L4 = 0x4;
+constexpr uint32_t FR_SEC_SHARED = 0x8;
+
+// A u16 stored raw at byte o (0 <= o <= 4N - 2, any parity) of N dwords.
+template <int N>
+__device__ __forceinline__ void fr_patch16(uint32_t (&v)[N], uint32_t o, uint32_t c) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int sh = 8 * ((int)o - 4 * k);
+        if (sh >= -8 && sh <= 24) {
+            const uint32_t val = sh < 0 ? (c >> 8) : (c << sh);
+            const uint32_t m = sh < 0 ? 0xffu : (0xffffu << sh);
+            v[k] = (v[k] & ~m) | (val & m);
+        }
+    }
+}
+
+// The SEC-byte block at `sa` (SEC-aligned, inside one frame) rewritten whole
+// with one or two checksum fields patched in: loaded, patched, stored back
+// with nontemporal 16-B stores.  The other bytes are the frame's own, which
+// nothing else writes during the call, so they are stored back unchanged.
+template <int SEC>
+__device__ __forceinline__ void fr_block_put(uint64_t sa, uint32_t o0, uint32_t c0, bool two, uint32_t o1,
+                                             uint32_t c1) {
+    constexpr int NQ = SEC / 16;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) v4u gv4u;
+    v4u q[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) q[k] = *reinterpret_cast<gv4u*>(sa + 16u * k);
+    uint32_t v[4 * NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        v[4 * k] = q[k].x;
+        v[4 * k + 1] = q[k].y;
+        v[4 * k + 2] = q[k].z;
+        v[4 * k + 3] = q[k].w;
+    }
+    fr_patch16<4 * NQ>(v, o0, c0);
+    if (two) fr_patch16<4 * NQ>(v, o1, c1);
+#pragma unroll
+    for (int k = 0; k < NQ; ++k)
+        __builtin_nontemporal_store(v4u{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]},
+                                    reinterpret_cast<gv4u*>(sa + 16u * k));
+}
+
+// A u16 field stored raw at `a` with an explicit cache policy (TX: FrameSrc's
+// STP): 2 sc0, 3 sc1, 4 sc0 sc1, 5 nt sc1, 6 nt sc0 sc1 (the product's;
+// vector stores, an odd address takes two byte stores).
+template <int STP>
+__device__ __forceinline__ void fr_store16_pol(uint64_t a, uint32_t c) {
+#define LVLIP_ST(BITS)                                                                                      \
+    if (a & 1ull) {                                                                                         \
+        const uint32_t hi = c >> 8;                                                                         \
+        asm volatile("global_store_byte %0, %1, off " BITS "\n\tglobal_store_byte %2, %3, off " BITS         \
+                     ::"v"(a), "v"(c), "v"(a + 1ull), "v"(hi) : "memory");                                  \
+    } else {                                                                                                \
+        asm volatile("global_store_short %0, %1, off " BITS ::"v"(a), "v"(c) : "memory");                    \
+    }
+    if constexpr (STP == 2) { LVLIP_ST("sc0") }
+    else if constexpr (STP == 3) { LVLIP_ST("sc1") }
+    else if constexpr (STP == 4) { LVLIP_ST("sc0 sc1") }
+    else if constexpr (STP == 5) { LVLIP_ST("nt sc1") }
+    else { LVLIP_ST("nt sc0 sc1") }
+#undef LVLIP_ST
+}
+
 // The decisions are those of skb_batch.c (host), which cites the reference line
 // of each.  Entry slots: RX with L4 and TX use two per frame (lanes 2f, 2f+1 of
 // one wave, so the pair exchanges results by shuffle), RX header-only one.  An
 // entry the frame does not have is empty (len 0).  Header bytes come from the
 // FrWin window; a field outside it is read with byte loads, never past the
 // frame's len.
-template <int MODE>
+// SEC (TX, lab A/B): 0 = each field stored as 2 bytes; 32 / 64 = the aligned
+// SEC-byte block around a field is rewritten whole when it lies inside the
+// frame (no partial-sector write reaches the memory side), 2-B stores
+// otherwise.
+// STP (TX): 0 = the launcher's nt_store flag (nontemporal or plain stores,
+// lab A/B); 2-6 = fr_store16_pol's cache policies; the product's TX fill
+// stores `nt sc0 sc1` (6).
+template <int MODE, int SEC = 0, int STP = 0>
 struct FrameSrc {
+    static_assert(SEC == 0 || SEC == 32 || SEC == 64, "field block size");
+    static_assert(STP == 0 || (STP >= 2 && STP <= 6), "field store policy");
     const uint8_t* base;             // the frames' bytes
     uint8_t* wbase;                  // the same, writable (TX)
     const lvlip_frame_desc* frames;  // this launch's first frame
@@ -247,6 +328,18 @@ struct FrameSrc {
         }
         d0 = fr_mk(fd.offset + FR_ETH, ihl * 4u, 0u - x.le16(24));  // src/ip_output.c:42,53
         w |= 1u;
+        if constexpr (SEC > 0) {
+            // which fields' SEC-byte blocks lie wholly inside [frame, frame + len)
+            const uint64_t fs = reinterpret_cast<uint64_t>(h), fe = fs + fd.len;
+            const uint64_t fh = fs + FR_ETH + 10u, bh = fh & ~(uint64_t)(SEC - 1);
+            if (bh >= fs && bh + SEC <= fe) w |= FR_SEC_HDR;
+            if (w & FR_HAS_L4) {
+                const uint64_t fl = fs + l4 + ((w >> 16) & 0xffu), bl = fl & ~(uint64_t)(SEC - 1);
+                if (bl >= fs && bl + SEC <= fe) w |= FR_SEC_L4;
+                if (bl == bh && (w & FR_SEC_HDR)) w |= FR_SEC_SHARED;
+                w |= (uint32_t)(fl - fh) << 24;  // <= 60 + 16 - 10
+            }
+        }
     }
 
     __device__ __forceinline__ lvlip_csum_desc get(uint32_t i, uint32_t& w, uint4* win = nullptr,
@@ -294,13 +387,29 @@ struct FrameSrc {
                                         uint64_t addr) const {
         const uint32_t f = i / SLOTS;
         if (MODE == FR_TX) {
+            // SEC: the header lane writes a block both fields share, so it
+            // takes the L4 lane's result (every lane runs the shuffle)
+            const uint32_t cl4 = SEC > 0 ? ((uint32_t)__shfl_xor((int)c, 1, 64) & 0xffffu) : 0u;
             if (!valid) return;
             if ((i & 1u) == 0u && out8) out8[f] = (uint8_t)(w & 1u);
             if (!(w & 1u)) return;
             const bool l4 = (i & 1u) != 0u;
             if (l4 && !(w & FR_HAS_L4)) return;
             // raw store (no htons) of the two bytes; one u16 store when aligned
-            const uint64_t fa = addr + (l4 ? (w >> 16) : 10u);
+            const uint64_t fa = addr + (l4 ? ((w >> 16) & 0xffu) : 10u);
+            if constexpr (SEC > 0) {
+                if (w & (l4 ? FR_SEC_L4 : FR_SEC_HDR)) {
+                    if (l4 && (w & FR_SEC_SHARED)) return;  // written by the header lane
+                    const uint64_t sa = fa & ~(uint64_t)(SEC - 1);
+                    const bool two = !l4 && (w & FR_SEC_SHARED);
+                    fr_block_put<SEC>(sa, (uint32_t)(fa - sa), c, two, (uint32_t)(fa - sa) + (w >> 24), cl4);
+                    return;
+                }
+            }
+            if constexpr (STP > 0) {
+                fr_store16_pol<STP>(fa, c);
+                return;
+            }
             uint8_t* p = wbase + (fa - reinterpret_cast<uint64_t>(base));
             if (nt_store) {
                 if (fa & 1ull) {

@@ -411,6 +411,90 @@ extern "C" int lvlip_lab_probe_tl(const void* src, uint64_t bytes, uint32_t* sin
     return -1;
 }
 
+// ---- scattered field-store probe (round 4, VERDICT r03 Next #1) ----------------
+// One lane per frame of a frame-descriptor array (16 B: offset u64, len u32,
+// pad): the TX fill's two checksum fields at frame + 24 and frame + 50 (ihl 5,
+// TCP), written on their own with nothing else running.  The buffer is
+// scratch (modes 0, 3 and 5 store constants).
+//   0  two 2-B nontemporal stores (the product's field stores)
+//   1  two 2-B loads, then the same bytes stored back nontemporally
+//   2  the aligned 32-B sector around each field loaded and stored back whole
+//      (nontemporal), once when both fields share it
+//   3  the same sectors stored whole without the load (constants)
+//   4  the aligned 64-B blocks, loaded and stored back whole
+//   5  two 2-B plain (temporal) stores
+//   6-10  two 2-B stores with cache policy sc0 / sc1 / sc0 sc1 / nt sc1 / nt sc0 sc1
+namespace {
+typedef unsigned int pv4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) pv4 gpv4;
+
+// salt: 0 at run time, unknown to the compiler (a load stored back unchanged
+// would otherwise be removed together with its store)
+template <int NQ, bool LOAD>
+__device__ __forceinline__ void probe_block(uint64_t a, uint32_t salt) {
+    pv4 q[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k)
+        q[k] = LOAD ? (*reinterpret_cast<gpv4*>(a + 16u * k) ^ pv4{salt, salt, salt, salt}) : pv4{1u, 2u, 3u, 4u};
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) __builtin_nontemporal_store(q[k], reinterpret_cast<gpv4*>(a + 16u * k));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_probe_fields(uint8_t* __restrict__ buf, const uint4* __restrict__ fd,
+                                                      uint32_t n, uint32_t salt) {
+    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
+    if (f >= n) return;
+    const uint4 d = fd[f];
+    const uint64_t fs = reinterpret_cast<uint64_t>(buf) + (((uint64_t)d.y << 32) | d.x);
+    const uint64_t a0 = fs + 24u, a1 = fs + 50u;
+    typedef __attribute__((address_space(1))) uint16_t gu16;
+    if (MODE == 0 || MODE == 5) {
+        if (MODE == 0) {
+            __builtin_nontemporal_store((uint16_t)f, reinterpret_cast<gu16*>(a0));
+            __builtin_nontemporal_store((uint16_t)f, reinterpret_cast<gu16*>(a1));
+        } else {
+            *reinterpret_cast<gu16*>(a0) = (uint16_t)f;
+            *reinterpret_cast<gu16*>(a1) = (uint16_t)f;
+        }
+    } else if (MODE == 1) {
+        const uint16_t x0 = *reinterpret_cast<gu16*>(a0) ^ (uint16_t)salt;
+        const uint16_t x1 = *reinterpret_cast<gu16*>(a1) ^ (uint16_t)salt;
+        __builtin_nontemporal_store(x0, reinterpret_cast<gu16*>(a0));
+        __builtin_nontemporal_store(x1, reinterpret_cast<gu16*>(a1));
+    } else if (MODE >= 6) {
+        // 2-B stores with an explicit cache policy: 6 sc0, 7 sc1, 8 sc0 sc1,
+        // 9 nt sc1, 10 nt sc0 sc1
+        const uint32_t v = f & 0xffffu;
+#define PST(BITS) asm volatile("global_store_short %0, %2, off " BITS "\n\tglobal_store_short %1, %2, off " BITS \
+                               ::"v"(a0), "v"(a1), "v"(v) : "memory")
+        if (MODE == 6) PST("sc0");
+        else if (MODE == 7) PST("sc1");
+        else if (MODE == 8) PST("sc0 sc1");
+        else if (MODE == 9) PST("nt sc1");
+        else PST("nt sc0 sc1");
+#undef PST
+    } else {
+        constexpr uint64_t B = MODE == 4 ? 64u : 32u;
+        constexpr int NQ = (int)(B / 16u);
+        const uint64_t s0 = a0 & ~(B - 1u), s1 = a1 & ~(B - 1u);
+        probe_block<NQ, MODE != 3>(s0, salt);
+        if (s1 != s0) probe_block<NQ, MODE != 3>(s1, salt);
+    }
+}
+}  // namespace
+
+extern "C" int lvlip_lab_probe_fields(void* buf, const void* frames, uint32_t n, int mode, void* stream) {
+    if (!buf || !frames) return -1;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 g((n + 255u) / 256u), b(256);
+#define PF(M) \
+    if (mode == M) { hipLaunchKernelGGL(k_probe_fields<M>, g, b, 0, s, (uint8_t*)buf, (const uint4*)frames, n, 0u); return hipGetLastError() == hipSuccess ? 0 : -3; }
+    PF(0) PF(1) PF(2) PF(3) PF(4) PF(5) PF(6) PF(7) PF(8) PF(9) PF(10)
+#undef PF
+    return -1;
+}
+
 // ---- cross-XCD atomicity probe -----------------------------------------------
 // Every wave's lane 0 takes K tickets from one counter: MODE 0 agent-scope
 // atomicAdd (global_atomic_add ... sc0), MODE 1 system scope (... sc0 sc1),

@@ -32,17 +32,17 @@ OK, EINVAL, ENODEV, EHIP, ENOMEM, ERANGE = 0, -1, -2, -3, -4, -5
 KERNEL_AUTO, KERNEL_FLAT, KERNEL_WINDOW, KERNEL_LANE = 0, 3, 8, 10
 # the A/B variants measured against them, in liblvlip_lab.so (lab_kernels.hip);
 # batch_dev sends these ids (and FLAT's A/B shapes) there, the product
-# returns EINVAL for them.  6 and 7 are retired round-1 ids (EINVAL everywhere).
-KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_WAVE_SIMPLE, KERNEL_FLAT_V1, KERNEL_WFLAT = 1, 2, 4, 5, 9
-KERNEL_RFLAT, KERNEL_WSFLAT, KERNEL_FLAT_OCC, KERNEL_FLAT_PERM, KERNEL_WINDOW_DYN = 11, 12, 13, 14, 15
-LAB_KERNELS = (KERNEL_WAVE, KERNEL_WAVE_LDS, KERNEL_WAVE_SIMPLE, KERNEL_FLAT_V1, KERNEL_WFLAT, KERNEL_RFLAT,
-               KERNEL_WSFLAT, KERNEL_FLAT_OCC, KERNEL_FLAT_PERM, KERNEL_WINDOW_DYN)
+# returns EINVAL for them.
+KERNEL_WAVE, KERNEL_WFLAT, KERNEL_FLAT_OCC = 1, 9, 13
+LAB_KERNELS = (KERNEL_WAVE, KERNEL_WFLAT, KERNEL_FLAT_OCC)
+# retired ids (EINVAL in both libraries): 6 and 7 (round 1's balanced stream
+# kernels), and the lab kernels pruned in round 4 after losing their A/Bs by
+# >= 3 % (k_wave_lds 2, k_wave_simple 4, k_flat v1 5, k_rflat 11, k_wsflat 12,
+# k_flat2_perm 14, k_window_dyn 15; DESIGN.md §4, last in commit 4e633d9)
+RETIRED_KERNELS = (2, 4, 5, 6, 7, 11, 12, 14, 15)
 REG_DMA, REG_ZEROCOPY = 0, 1
-KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "wave_lds": KERNEL_WAVE_LDS,
-                "flat": KERNEL_FLAT, "wave_simple": KERNEL_WAVE_SIMPLE, "flat_v1": KERNEL_FLAT_V1,
-                "window": KERNEL_WINDOW, "wflat": KERNEL_WFLAT, "lane": KERNEL_LANE,
-                "rflat": KERNEL_RFLAT, "wsflat": KERNEL_WSFLAT, "flat_occ": KERNEL_FLAT_OCC,
-                "flat_perm": KERNEL_FLAT_PERM, "window_dyn": KERNEL_WINDOW_DYN}
+KERNEL_NAMES = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "flat": KERNEL_FLAT, "window": KERNEL_WINDOW,
+                "wflat": KERNEL_WFLAT, "lane": KERNEL_LANE, "flat_occ": KERNEL_FLAT_OCC}
 KERNEL_LABELS = {v: k for k, v in KERNEL_NAMES.items()}
 
 # struct lvlip_csum_desc {u64 offset; i32 len; u32 start_sum;}  (16 B)
@@ -85,6 +85,7 @@ class Frame(ctypes.Structure):  # include/lvlip_skb.h: lvlip_frame
 RX_OK, RX_NOT_IP, RX_SHORT, RX_BAD_VERSION, RX_BAD_IHL, RX_TTL0, RX_BAD_CSUM, RX_BAD_L4, \
     RX_UNKNOWN_PROTO = range(1, 10)
 RX_VERIFY_L4 = 0x1
+ECHO_FULL = 0x1  # lvlip_icmp_echo_reply_dev_ex (include/lvlip_skb.h)
 PLAN_MALFORMED = 0xFFFFFFFF
 
 
@@ -119,30 +120,43 @@ def _load(path: str) -> ctypes.CDLL:
 BUILD_SOURCES = os.path.join(HERE, "BUILD_SOURCES")
 
 
-def source_build_id() -> str:
-    """SHA-256 (first 16 hex digits) of the product's sources in the tree, in
-    the order BUILD_SOURCES lists them: what level-ip_amd/Makefile compiles into
-    lvlip_build_id()."""
+def source_build_id(list_file: str = BUILD_SOURCES) -> str:
+    """SHA-256 (first 16 hex digits) of the sources a list file names, in its
+    order: BUILD_SOURCES (the product, lvlip_build_id()), LAB_SOURCES or
+    TESTKIT_SOURCES (the helper libraries' stamps) -- what
+    level-ip_amd/Makefile compiles into each library."""
     import hashlib
 
     root = os.path.dirname(HERE)
     h = hashlib.sha256()
-    with open(BUILD_SOURCES) as f:
+    with open(list_file) as f:
         for rel in f.read().split():
             with open(os.path.join(root, rel), "rb") as g:
                 h.update(g.read())
     return h.hexdigest()[:16]
 
 
+def _stamp(lib: ctypes.CDLL, path: str, symbol: str, list_file: str) -> str:
+    """The library's build stamp, checked against the tree's sources; a
+    library without the symbol (built before stamps existed) or with another
+    stamp is stale and refused."""
+    try:
+        fn = getattr(lib, symbol)
+    except AttributeError:
+        raise LvlipUnavailable(f"{path} has no {symbol} (built before build stamps): rebuild with "
+                               "`make -C level-ip_amd`") from None
+    fn.restype = ctypes.c_char_p
+    fn.argtypes = []
+    got, want = fn().decode(), source_build_id(list_file)
+    if got != want:
+        raise LvlipUnavailable(f"{path} was built from other sources (stamp {got}, tree {want}): "
+                               "rebuild with `make -C level-ip_amd`")
+    return got
+
+
 _share_torch_hip_runtime()
 _lib = _load(LIB_PATH)
-_lib.lvlip_build_id.restype = ctypes.c_char_p
-_lib.lvlip_build_id.argtypes = []
-BUILD_ID = _lib.lvlip_build_id().decode()
-if BUILD_ID != source_build_id():
-    raise LvlipUnavailable(
-        f"{LIB_PATH} was built from other sources (build id {BUILD_ID}, tree "
-        f"{source_build_id()}): rebuild with `make -C level-ip_amd`")
+BUILD_ID = _stamp(_lib, LIB_PATH, "lvlip_build_id", BUILD_SOURCES)
 
 # every entry point declared in include/lvlip_csum.h, with its ctypes signature
 SIGNATURES = {
@@ -194,6 +208,14 @@ SIGNATURES = {
                                                ctypes.c_uint16]),
     "lvlip_icmp_echo_reply_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                  ctypes.c_void_p, ctypes.c_void_p]),
+    "lvlip_icmp_echo_reply_dev_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                    ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    # Group 4: one batch over several GPUs
+    "lvlip_partition_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_void_p]),
+    "lvlip_csum_batch_host_flat_multi": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                                        ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32,
+                                                        ctypes.c_void_p]),
     "lvlip_rx_verify_skb_list": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                 ctypes.c_void_p, ctypes.c_uint32]),
     "lvlip_tx_checksum_skb_list": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
@@ -479,17 +501,48 @@ def tx_checksum_dev(base, fdescs, stream=None):
     return status[:n]
 
 
-def icmp_echo_reply_dev(base, fdescs, stream=None):
-    """lvlip_icmp_echo_reply_dev (f4) in place on frames in a CUDA uint8 tensor;
-    returns the per-frame status (1 updated, 2 recomputed, 0 untouched)."""
+def icmp_echo_reply_dev(base, fdescs, stream=None, flags: int = 0):
+    """lvlip_icmp_echo_reply_dev[_ex] (f4) in place on frames in a CUDA uint8
+    tensor; returns the per-frame status (1 updated, 2 recomputed, 0
+    untouched).  flags 0: the RFC 1624 update, exact for requests whose ICMP
+    checksum verified (the caller's precondition); ECHO_FULL: icmpv4_reply's
+    full recomputation for any request."""
     import torch
 
     n, fd = _frames_dev(base, fdescs)
     status = torch.empty(max(n, 1), dtype=torch.uint8, device=base.device)
     s = stream or torch.cuda.current_stream(base.device)
-    _check(_lib.lvlip_icmp_echo_reply_dev(base.data_ptr(), fd.data_ptr(), n, status.data_ptr(),
-                                          s.cuda_stream), "lvlip_icmp_echo_reply_dev")
+    if flags == 0:
+        rc = _lib.lvlip_icmp_echo_reply_dev(base.data_ptr(), fd.data_ptr(), n, status.data_ptr(), s.cuda_stream)
+    else:
+        rc = _lib.lvlip_icmp_echo_reply_dev_ex(base.data_ptr(), fd.data_ptr(), n, flags, status.data_ptr(),
+                                               s.cuda_stream)
+    _check(rc, "lvlip_icmp_echo_reply_dev")
     return status[:n]
+
+
+# ----------------------------------------------------- Group 4: several GPUs --
+
+def partition_bytes(descs: np.ndarray, parts: int) -> list:
+    """lvlip_partition_bytes: cuts[0..parts] of the byte-balanced contiguous
+    partition (part p = descriptors [cuts[p], cuts[p+1]))."""
+    d = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    cuts = np.zeros(parts + 1, dtype=np.uint32)
+    _check(_lib.lvlip_partition_bytes(d.ctypes.data if d.size else None, d.size, parts, cuts.ctypes.data),
+           "lvlip_partition_bytes")
+    return [int(c) for c in cuts]
+
+
+def batch_host_flat_multi(ctxs, base: np.ndarray, descs: np.ndarray) -> np.ndarray:
+    """lvlip_csum_batch_host_flat_multi over Contexts (one per device, or
+    several on one device), one host thread each."""
+    base = _as_u8(base)
+    d = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    out = np.empty(d.size, dtype=np.uint16)
+    _check(_lib.lvlip_csum_batch_host_flat_multi(arr, len(ctxs), base.ctypes.data, base.size, d.ctypes.data,
+                                                 d.size, out.ctypes.data), "lvlip_csum_batch_host_flat_multi")
+    return out
 
 
 def frames_variant_dev(mode: int, variant: int, base, fdescs, stream=None):
@@ -619,6 +672,7 @@ def testkit() -> ctypes.CDLL:
     global _testkit
     if _testkit is None:
         tk = _load(TESTKIT_PATH)
+        _stamp(tk, TESTKIT_PATH, "lvlip_testkit_build_id", os.path.join(HERE, "TESTKIT_SOURCES"))
         tk.lvlip_testkit_fill.restype = ctypes.c_int
         tk.lvlip_testkit_fill.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                           ctypes.c_uint64, ctypes.c_void_p]
@@ -637,6 +691,7 @@ def lab() -> ctypes.CDLL:
     global _lab
     if _lab is None:
         lb = _load(LAB_PATH)
+        _stamp(lb, LAB_PATH, "lvlip_lab_build_id", os.path.join(HERE, "LAB_SOURCES"))
         lb.lvlip_lab_probe.restype = ctypes.c_int
         lb.lvlip_lab_probe.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -13,7 +13,10 @@ descriptor ranges with no exchange on the data path:
                            kernel
   gather_results(...)      results back in batch order (torch.distributed
                            all_gather: RCCL on GPUs, gloo on CPU tests), 2 bytes
-                           per packet
+                           per packet on the wire
+
+The C-ABI has the same partition (lvlip_partition_bytes, include/lvlip_csum.h
+Group 4) for a level-ip daemon that shards over the node's GPUs from threads.
 
 bench.py's weak-scaling run does not move packets at all: each rank
 generates its own shard of the stream (workloads.make(first=rank*n)).
@@ -70,12 +73,13 @@ def gather_results(local_out, counts: list[int], group=None):
 
     world = dist.get_world_size(group)
     m = max(counts) if counts else 0
-    # carried as int32 (gloo has no 16-bit integer collectives); bit pattern kept
-    buf = torch.zeros(m, dtype=torch.int32, device=local_out.device)
-    buf[: local_out.numel()] = local_out.view(torch.int16).to(torch.int32) & 0xFFFF
+    # carried as their 2 bytes each (uint8: RCCL and gloo both gather bytes;
+    # gloo has no 16-bit integer collective), bit pattern kept
+    buf = torch.zeros(2 * m, dtype=torch.uint8, device=local_out.device)
+    buf[: 2 * local_out.numel()] = local_out.contiguous().view(torch.int16).view(torch.uint8)
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
-    return torch.cat([p[:c] for p, c in zip(parts, counts)]).to(torch.int16)
+    return torch.cat([p[: 2 * c] for p, c in zip(parts, counts)]).view(torch.int16)
 
 
 def scatter_from_root(buf, descs, device, group=None, root: int = 0):

@@ -1,0 +1,60 @@
+#!/usr/bin/env bash
+# One runner for the GPU box (through gpurun): each named step runs under its
+# own time limit, output under gpurun_out/; the first step that fails (or
+# faults, or times out) ends the script with its status.  Replaces round 3's
+# single-use scripts/*_once.sh wrappers.
+#
+#   bash scripts/gpu_steps.sh STEP [STEP ...]
+#
+# Steps:
+#   tests                 pytest -m gpu (one process, per-test timeout)
+#   smoke                 __graft_entry__.smoke()
+#   bench[:WL]            the default bench line (WL: tcp1500 | tcp9000 | mixed)
+#   txstore               scripts/lab_tx_store.py (TX field-store A/B + probes)
+#   txpmc                 FETCH_SIZE / WRITE_SIZE passes of the TX variants
+#   modes:K               K processes of scripts/lab_modes.py (mixed line modes)
+#   evidence:WL           scripts/evidence.sh for WL (bench + trace + PMC)
+#   ab:WL:VARIANTS        scripts/ab.py on WL with a variant list (AB_VARIANTS syntax, no ':' inside
+#                         a variant here: use AB_VARIANTS directly for those)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${TAG:-r04}
+
+run() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($secs s): $*"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -25 "gpurun_out/$name.log"
+  echo "== $name rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+}
+
+for step in "$@"; do
+  case "$step" in
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 300 python bench.py ;;
+    bench:*) wl=${step#bench:}; run "bench_$wl" 300 python bench.py --workload "$wl" ;;
+    txstore) run txstore 400 python scripts/lab_tx_store.py "gpurun_out/${TAG}_tx_store.json" 7 ;;
+    txpmc)
+      for v in ${TXPMC_VARIANTS:-tx_product tx_plain rx_l4}; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          run "txpmc_${v}_$c" 180 /opt/rocm/bin/rocprofv3 --pmc "$c" --kernel-include-regex "k_flat2|k_probe" \
+            --output-format csv -d "gpurun_out/txpmc/${v}_$c" -o "${v}_$c" -- python3 scripts/lab_tx_store.py --only "$v" 20
+        done
+      done
+      run txtrace 180 /opt/rocm/bin/rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/txpmc/trace \
+        -o trace -- python3 scripts/lab_tx_store.py --only tx_product 20 ;;
+    modes:*)
+      k=${step#modes:}
+      for i in $(seq 1 "$k"); do run "modes_p$i" 240 python scripts/lab_modes.py "gpurun_out/${TAG}_modes_p$i.json"; done ;;
+    evidence:*) wl=${step#evidence:}; run "evidence_$wl" 900 env TAG="$TAG" WL="$wl" bash scripts/evidence.sh ;;
+    ab:*) IFS=: read -r _ wl vars <<< "$step"
+      run "ab_$wl" 600 env AB_WORKLOAD="$wl" AB_VARIANTS="$vars" python scripts/ab.py "gpurun_out/${TAG}_ab_$wl.json" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "all steps ok: $*"

@@ -51,7 +51,7 @@ def main():
     ck = [("csum", k, u, w) for k, u, w in [
         ("wave", 2, 4), ("wave", 2, 8), ("wave", 2, 12), ("wave", 2, 16), ("wave", 2, 24),
         ("wave", 3, 8), ("wave", 3, 12), ("wave", 3, 16), ("wave", 4, 8), ("wave", 4, 16),
-        ("wave_simple", 2, 0), ("wave_lds", 2, 0), ("flat", 0, 0)]]
+        ("flat", 0, 0)]]
     res = {}
     for rnd in range(3):
         for v in variants:

@@ -65,19 +65,10 @@ def main():
     nw = 0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
-    dyn = os.environ.get("TAIL_DYN") == "1"  # k_window_dyn (one workgroup of wpb waves per CU)
-    if dyn:
-        lab.lvlip_lab_window_dyn.restype = ctypes.c_int
-        lab.lvlip_lab_window_dyn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
-                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
-                                             ctypes.c_void_p]
+    dyn = False  # k_window_dyn (TAIL_DYN=1) was pruned in round 4 (last in commit 4e633d9)
     for k in range(launches):
-        if dyn:
-            nw = lab.lvlip_lab_window_dyn(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
-                                          stamps[k].data_ptr(), nbytes, wpb, 2 | (4 << 8), s.cuda_stream)
-        else:
-            nw = lab.lvlip_lab_window_stamps(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
-                                             stamps[k].data_ptr(), nbytes, wpc, wpb, s.cuda_stream)
+        nw = lab.lvlip_lab_window_stamps(base.data_ptr(), descs.data_ptr(), b.n, out.data_ptr(),
+                                         stamps[k].data_ptr(), nbytes, wpc, wpb, s.cuda_stream)
         assert nw > 0, nw
     e1.record(s)
     torch.cuda.synchronize()

@@ -12,43 +12,62 @@ for p in (PKG, ORACLE, ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-BUILD_CONTAINER = os.path.isdir("/root/reference")  # the GPU box has no reference tree
+def _may_rebuild() -> bool:
+    """Whether a stale library is rebuilt here or stops the run.
+    LVLIP_REBUILD=1 / 0 decides explicitly; by default a machine without a GPU
+    (no /dev/kfd: the build container) rebuilds, and a GPU box, which runs the
+    prebuilt snapshot and must not build inside a GPU run, refuses."""
+    e = os.environ.get("LVLIP_REBUILD")
+    if e in ("0", "1"):
+        return e == "1"
+    return not os.path.exists("/dev/kfd")
 
 
-def _source_build_id() -> str:
+def _source_build_id(list_name: str = "BUILD_SOURCES") -> str:
     """lvlip.source_build_id() without importing lvlip (which loads the library)."""
     import hashlib
 
     h = hashlib.sha256()
-    with open(os.path.join(PKG, "BUILD_SOURCES")) as f:
+    with open(os.path.join(PKG, list_name)) as f:
         for rel in f.read().split():
             with open(os.path.join(ROOT, rel), "rb") as g:
                 h.update(g.read())
     return h.hexdigest()[:16]
 
 
-def _library_current() -> bool:
-    """The product library carries the tree's source hash (lvlip_build_id(),
-    read from the file so that nothing loads the HIP runtime here)."""
-    so = os.path.join(PKG, "liblvlip_csum.so")
-    if not os.path.exists(so) or not os.path.exists(os.path.join(PKG, "liblvlip_testkit.so")):
-        return False
-    with open(so, "rb") as f:
-        return _source_build_id().encode() in f.read()
+STAMPED = (("liblvlip_csum.so", "BUILD_SOURCES"), ("liblvlip_testkit.so", "TESTKIT_SOURCES"),
+           ("liblvlip_lab.so", "LAB_SOURCES"))
+
+
+def _libraries_current() -> list:
+    """The libraries whose stamp (the tree's source hash, read from the file so
+    that nothing loads the HIP runtime here) is missing or differs."""
+    stale = []
+    for so, lst in STAMPED:
+        path = os.path.join(PKG, so)
+        if not os.path.exists(path):
+            stale.append(so)
+            continue
+        with open(path, "rb") as f:
+            if _source_build_id(lst).encode() not in f.read():
+                stale.append(so)
+    return stale
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
-    # The product library must be built from this tree's sources.  The build
-    # container rebuilds it; anywhere else (the GPU box runs the prebuilt
-    # snapshot) a stale library stops the run instead of being tested.
-    if not _library_current():
-        if not BUILD_CONTAINER:
-            pytest.exit("liblvlip_csum.so was not built from this tree's sources (lvlip_build_id "
-                        "differs): run `make -C level-ip_amd` before testing", returncode=3)
+    # The libraries must be built from this tree's sources: rebuilt here when
+    # that is allowed (_may_rebuild), else a stale one stops the run instead
+    # of being tested.
+    stale = _libraries_current()
+    if stale:
+        if not _may_rebuild():
+            pytest.exit(f"{', '.join(stale)} not built from this tree's sources (build stamp differs): "
+                        "run `make -C level-ip_amd` before testing (or set LVLIP_REBUILD=1)", returncode=3)
         subprocess.run(["make", "-s", "-C", PKG, "-j8"], check=True)
-        if not _library_current():
-            pytest.exit("liblvlip_csum.so still differs from the tree after make", returncode=3)
+        stale = _libraries_current()
+        if stale:
+            pytest.exit(f"{', '.join(stale)} still differ from the tree after make", returncode=3)
     subprocess.run(["make", "-s", "-C", ORACLE, "oracle"], check=True)
 
 

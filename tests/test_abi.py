@@ -63,7 +63,7 @@ def test_header_is_plain_c():
 def test_desc_layout():
     assert lvlip.DESC_DTYPE.itemsize == 16
     assert ctypes.sizeof(lvlip.LaunchCfg) == 16
-    assert lvlip.lib().lvlip_abi_version() == 1
+    assert lvlip.lib().lvlip_abi_version() == 2
 
 
 def test_error_paths_without_gpu():
@@ -127,3 +127,23 @@ def test_auto_selection_table():
     # flat batch up to 2^30 descriptors
     assert lvlip.batch_launches(0) == 0
     assert lvlip.batch_launches(1 << 20, lvlip.KERNEL_FLAT, len_hint=391) == 1
+
+
+def test_stale_or_unstamped_helper_library_refused(tmp_path):
+    """VERDICT r03 Next #6 / ADVICE r03: the lab and testkit libraries carry
+    source stamps like the product; a library without the stamp symbol (built
+    before stamps) or with another stamp raises LvlipUnavailable with the
+    rebuild hint instead of running stale A/B code."""
+    libc = ctypes.CDLL("libc.so.6")
+    with pytest.raises(lvlip.LvlipUnavailable, match="no lvlip_lab_build_id"):
+        lvlip._stamp(libc, "libc.so.6", "lvlip_lab_build_id", os.path.join(lvlip.HERE, "LAB_SOURCES"))
+    other = tmp_path / "SOURCES"
+    other.write_text("include/lvlip_csum.h\n")
+    lab = ctypes.CDLL(lvlip.LAB_PATH)
+    with pytest.raises(lvlip.LvlipUnavailable, match="other sources"):
+        lvlip._stamp(lab, lvlip.LAB_PATH, "lvlip_lab_build_id", str(other))
+    # the tree's own builds pass
+    assert lvlip.lab() is not None and lvlip.testkit() is not None
+    for so, lst in (("liblvlip_lab.so", "LAB_SOURCES"), ("liblvlip_testkit.so", "TESTKIT_SOURCES")):
+        assert lvlip.source_build_id(os.path.join(lvlip.HERE, lst)).encode() in open(
+            os.path.join(lvlip.HERE, so), "rb").read()

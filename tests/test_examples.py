@@ -57,3 +57,28 @@ def test_install_and_build_against_it(tmp_path):
     assert r.returncode == 0, r.stderr
     r = subprocess.run(["ldd", str(exe)], capture_output=True, text=True)
     assert str(prefix / "lib" / "liblvlip_csum.so") in r.stdout, r.stdout
+
+
+MULTI = os.path.join(ROOT, "examples", "build", "multi_gpu")
+
+
+def test_multi_gpu_example_fails_loudly_without_gpu():
+    import lvlip
+
+    if lvlip.device_count() > 0:
+        pytest.skip("a GPU is present")
+    _exe()
+    r = subprocess.run([MULTI, "64", "2"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "no HIP device" in r.stderr, (r.returncode, r.stderr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("contexts", [2, 4])
+def test_example_multi_gpu(contexts):
+    """thread per context (on one GPU here: context k on
+    device k % device_count), by the library and by hand with pthreads, every
+    result against the per-call checksum()."""
+    assert os.path.exists(MULTI), "examples/build/multi_gpu not built (run __graft_entry__.build())"
+    r = subprocess.run([MULTI, "65536", str(contexts)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert f"over {contexts} contexts" in r.stdout, r.stdout

@@ -29,12 +29,6 @@ VARIANTS = [
     (lvlip.KERNEL_WAVE, 4, 0),
     (lvlip.KERNEL_WAVE, 2, 1),     # 1 wave/CU: long per-wave ranges, window refills
     (lvlip.KERNEL_WAVE, 4, 24),
-    (lvlip.KERNEL_WAVE_SIMPLE, 1, 0),
-    (lvlip.KERNEL_WAVE_SIMPLE, 2, 0),
-    (lvlip.KERNEL_WAVE_SIMPLE, 4, 8),
-    (lvlip.KERNEL_WAVE_LDS, 1, 0),
-    (lvlip.KERNEL_WAVE_LDS, 2, 0),
-    (lvlip.KERNEL_WAVE_LDS, 4, 8),
     (lvlip.KERNEL_FLAT, 0, 0),
     (lvlip.KERNEL_FLAT, 2, 0),
     (lvlip.KERNEL_FLAT, 8, 0),
@@ -49,7 +43,6 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT, 4 | (1 << 11), 0),
     (lvlip.KERNEL_FLAT, 6 | (1 << 11), 0),
     (lvlip.KERNEL_FLAT, 8 | (1 << 11), 0),
-    (5, 0, 0),                     # first-generation flat kernel (A/B)
     (lvlip.KERNEL_WINDOW, 3, 0),   # interleaved stream: groups dealt round robin
     (lvlip.KERNEL_WINDOW, 2, 1),   # 1 wave/CU: long per-wave sequences, window refills
     (lvlip.KERNEL_WINDOW, 4, 24),
@@ -60,13 +53,6 @@ VARIANTS = [
     (lvlip.KERNEL_LANE, 2 | (6 << 8) | (1 << 16), 0),
     (lvlip.KERNEL_LANE, 8 | (1 << 8) | (4 << 16), 0),
     (lvlip.KERNEL_LANE, 4 | (2 << 8) | (8 << 16), 0),
-    (lvlip.KERNEL_RFLAT, 0, 0),    # flat sweep per wave, tiles dealt round robin, ring
-    (lvlip.KERNEL_RFLAT, 2 | (32 << 8), 1),
-    (lvlip.KERNEL_RFLAT, 8 | (64 << 8), 16),
-    (lvlip.KERNEL_RFLAT, 6 | (16 << 8), 4),
-    (lvlip.KERNEL_WSFLAT, 0, 0),   # sweeper waves + a planner wave, tiles double-buffered
-    (lvlip.KERNEL_WSFLAT, 2 | (1 << 8), 1),
-    (lvlip.KERNEL_WSFLAT, 8 | (4 << 8) | (1 << 12), 3),
     (lvlip.KERNEL_FLAT_OCC, 8 | (5 << 8) | (1 << 12), 0),  # k_flat2 at a set occupancy
     (lvlip.KERNEL_FLAT_OCC, 8 | (6 << 8), 0),
     (lvlip.KERNEL_FLAT_OCC, 6 | (7 << 8) | (1 << 12), 0),
@@ -76,10 +62,6 @@ VARIANTS = [
     (lvlip.KERNEL_FLAT_OCC, 0x4508 | (3 << 16), 0),  # + s_setprio around load issue and phase 1
     (lvlip.KERNEL_FLAT_OCC, 0x4508 | (4 << 16), 0),  # + last round dealt to all four waves
     (lvlip.KERNEL_FLAT_OCC, 0x4508 | (8 << 16), 0),  # + no early exit from a round
-    (lvlip.KERNEL_FLAT_PERM, 16 | (2 << 8) | (1 << 12), 0),  # run-dealt tile map (identity below a generation)
-    (lvlip.KERNEL_WINDOW_DYN, 2 | (4 << 8), 12),  # window deal, items claimed in the CU's workgroup
-    (lvlip.KERNEL_WINDOW_DYN, 2 | (1 << 8), 8),
-    (lvlip.KERNEL_WINDOW_DYN, 2 | (2 << 8), 12),
 ]
 VID = [f"k{k}-u{u}-w{w}" for k, u, w in VARIANTS]
 
@@ -252,23 +234,14 @@ def test_full_size_bit_exact(name):
     for variant in [(lvlip.KERNEL_WAVE, 4, 0), (lvlip.KERNEL_WAVE, 3, 4),
                     (lvlip.KERNEL_WINDOW, 3, 0), (lvlip.KERNEL_WINDOW, 2, 0),
                     (lvlip.KERNEL_WFLAT, 0, 0), (lvlip.KERNEL_WFLAT, 8 | (64 << 8), 16),
-                    (lvlip.KERNEL_RFLAT, 0, 0), (lvlip.KERNEL_RFLAT, 8 | (32 << 8), 8),
-                    (lvlip.KERNEL_WSFLAT, 0, 0), (lvlip.KERNEL_WSFLAT, 8 | (2 << 8), 3),
                     (lvlip.KERNEL_FLAT, 4 | (1 << 11), 0), (lvlip.KERNEL_FLAT, 8 | (1 << 11), 0),
-                    (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_FLAT, 0, 0), (lvlip.KERNEL_FLAT, 8, 0),
                     (lvlip.KERNEL_FLAT, 8 | (1 << 10), 0),
                     (lvlip.KERNEL_LANE, 0, 0), (lvlip.KERNEL_AUTO, 0, 0),
-                    # lab A/B variants of round 3: VAR bits of k_flat2_occ, and the
-                    # run-dealt tile maps (full generations of 640-1 280 x 256 here)
+                    # lab A/B variants of round 3: VAR bits of k_flat2_occ
                     (lvlip.KERNEL_FLAT_OCC, 0x4508 | (3 << 16), 0),
                     (lvlip.KERNEL_FLAT_OCC, 0x4508 | (4 << 16), 0),
-                    (lvlip.KERNEL_FLAT_OCC, 0x4508 | (8 << 16), 0),
-                    (lvlip.KERNEL_FLAT_PERM, 16 | (2 << 8) | (1 << 12), 0),
-                    (lvlip.KERNEL_FLAT_PERM, 16 | (2 << 8), 0),
-                    (lvlip.KERNEL_FLAT_PERM, 32 | (1 << 8) | (1 << 12), 0),
-                    (lvlip.KERNEL_FLAT_PERM, 64 | (2 << 8) | (1 << 12), 0),
-                    (lvlip.KERNEL_WINDOW_DYN, 2 | (4 << 8), 12), (lvlip.KERNEL_WINDOW_DYN, 2 | (2 << 8), 8)]:
+                    (lvlip.KERNEL_FLAT_OCC, 0x4508 | (8 << 16), 0)]:
         assert np.array_equal(run(base, descs, variant, out), want), variant
     # adversarial packets really are there and fold as the reference does
     ones = b.paint == 2
@@ -331,60 +304,6 @@ def test_wflat_tiles(tile):
             got = out.cpu().numpy().view(np.uint16)
             bad = np.nonzero(got != want[:n])[0]
             assert bad.size == 0, (n, u, wpc, bad[:5])
-
-
-# k_rflat: every built (group loads per round, descriptors per tile)
-RFLAT_SHAPES = [(2, 16), (4, 16), (6, 16), (8, 16), (2, 32), (4, 32), (6, 32), (8, 32), (4, 64), (8, 64)]
-
-
-@pytest.mark.parametrize("shape", RFLAT_SHAPES, ids=[f"u{u}d{d}" for u, d in RFLAT_SHAPES])
-def test_rflat_tiles(shape):
-    """k_rflat for every built shape: batch sizes that leave the last tile short
-    or give waves no tile, 1 and 24 waves/CU (long per-wave tile sequences, many
-    waves with one tile), ragged lengths with descriptors past the sweep cap
-    (64 KiB), empty and negative lengths at odd offsets; and batches of tiny
-    packets, whose one-group tiles run the issue side against its limit of
-    tile buffers; every output against the oracle."""
-    u, tile = shape
-    for seed, (base, d, want) in ((200 + u + tile, ragged_batch(200 + u + tile)),
-                                  (300 + u + tile, tiny_batch(300 + u + tile))):
-        for n in BATCH_SIZES:
-            descs = dev_descs(d[:n])
-            for wpc in (0, 1, 24):
-                out = lvlip.batch_torch(base, descs, kernel=lvlip.KERNEL_RFLAT, unroll=u | (tile << 8),
-                                        waves_per_cu=wpc)
-                torch.cuda.synchronize()
-                got = out.cpu().numpy().view(np.uint16)
-                bad = np.nonzero(got != want[:n])[0]
-                assert bad.size == 0, (seed, n, wpc, bad[:5])
-
-
-# k_wsflat: every built (group loads per round, descriptors per tile, order)
-WSFLAT_SHAPES = [(4, 64, 0), (4, 128, 0), (4, 256, 0), (8, 128, 0), (8, 256, 0), (8, 256, 1), (4, 256, 1),
-                 (2, 64, 0), (2, 128, 0)]
-
-
-@pytest.mark.parametrize("shape", WSFLAT_SHAPES, ids=[f"u{u}d{d}b{b}" for u, d, b in WSFLAT_SHAPES])
-def test_wsflat_tiles(shape):
-    """k_wsflat for every built shape: batch sizes that leave the last tile
-    short or give workgroups no tile, 1 and 3 workgroups/CU (long per-workgroup
-    tile sequences through both LDS buffers, and workgroups with one tile:
-    plan, sweep and finish with nothing to overlap), ragged lengths with
-    descriptors past the sweep cap (the planner's big-packet loop), empty and
-    negative lengths at odd offsets, and tiny packets; every output against the
-    oracle."""
-    u, tile, blocks = shape
-    code = u | ((tile // 64) << 8) | (blocks << 12)
-    for seed, (base, d, want) in ((400 + u + tile, ragged_batch(400 + u + tile)),
-                                  (500 + u + tile, tiny_batch(500 + u + tile))):
-        for n in BATCH_SIZES:
-            descs = dev_descs(d[:n])
-            for wpc in (0, 1, 3):
-                out = lvlip.batch_torch(base, descs, kernel=lvlip.KERNEL_WSFLAT, unroll=code, waves_per_cu=wpc)
-                torch.cuda.synchronize()
-                got = out.cpu().numpy().view(np.uint16)
-                bad = np.nonzero(got != want[:n])[0]
-                assert bad.size == 0, (seed, n, wpc, bad[:5])
 
 
 # (lanes per packet S, packets per group P, chunks per lane K): every built shape
@@ -585,10 +504,6 @@ def test_bad_launch_shapes_rejected():
                  (lvlip.KERNEL_LANE, 3), (lvlip.KERNEL_LANE, 4 | (5 << 8)),
                  (lvlip.KERNEL_LANE, 4 | (1 << 8) | (3 << 16)),
                  (lvlip.KERNEL_LANE, 4 | (1 << 8) | (1 << 25)),
-                 (lvlip.KERNEL_RFLAT, 3), (lvlip.KERNEL_RFLAT, 2 | (64 << 8)), (lvlip.KERNEL_RFLAT, 4 | (48 << 8)),
-                 (lvlip.KERNEL_RFLAT, 4 | (1 << 16)),
-                 (lvlip.KERNEL_WSFLAT, 3), (lvlip.KERNEL_WSFLAT, 2 | (4 << 8)), (lvlip.KERNEL_WSFLAT, 4 | (3 << 8)),
-                 (lvlip.KERNEL_WSFLAT, 4 | (1 << 13)),
                  (lvlip.KERNEL_FLAT_OCC, 8 | (7 << 8)), (lvlip.KERNEL_FLAT_OCC, 8 | (6 << 8) | (1 << 13)),
                  (lvlip.KERNEL_FLAT_OCC, 0)):
         with pytest.raises(lvlip.LvlipError):
@@ -618,7 +533,7 @@ def test_batch_launches_reports_the_split():
     assert lvlip.batch_launches(64 << 20, len_hint=1500) >= 8
     assert lvlip.batch_launches(1 << 20, lvlip.KERNEL_FLAT, len_hint=700) == 1
     assert lvlip.batch_launches(1 << 20, len_hint=20) == 1
-    assert lvlip.batch_launches(1 << 20, lvlip.KERNEL_WSFLAT) == 1
+    assert lvlip.batch_launches(1 << 20, lvlip.KERNEL_WFLAT) == 1
     n = 800_000
     rng = np.random.default_rng(77)
     host = rng.integers(0, 256, n * 64, dtype=np.uint8)
@@ -639,22 +554,23 @@ def test_batch_launches_reports_the_split():
 
 def test_retired_and_lab_ids_rejected_by_the_product():
     """The product library runs AUTO, FLAT (2, 4, 8 loads per round), WINDOW and
-    LANE only: the retired round-1 ids 6 and 7 and the lab's A/B ids return
-    LVLIP_EINVAL there (nothing launched), with no silent substitute."""
+    LANE only: the retired ids (round 1's 6 and 7, the lab kernels pruned in
+    round 4) and the lab's A/B ids return LVLIP_EINVAL there (nothing
+    launched), with no silent substitute; the retired ids are EINVAL in the lab
+    library too."""
     import ctypes
 
     base = torch.zeros(64, dtype=torch.uint8, device="cuda")
     descs = dev_descs(mk_descs([0], [4], [0]))
     out = torch.empty(1, dtype=torch.int16, device="cuda")
     L = lvlip.lib()
-    for k, u in ((6, 0), (7, 0), (lvlip.KERNEL_WAVE, 2), (lvlip.KERNEL_WAVE_LDS, 2),
-                 (lvlip.KERNEL_WAVE_SIMPLE, 2), (lvlip.KERNEL_FLAT_V1, 0), (lvlip.KERNEL_WFLAT, 0),
-                 (lvlip.KERNEL_FLAT, 6), (lvlip.KERNEL_FLAT, 4 | (2 << 8)), (lvlip.KERNEL_RFLAT, 0),
-                 (lvlip.KERNEL_WSFLAT, 0), (lvlip.KERNEL_FLAT_OCC, 8 | (6 << 8))):
+    for k, u in ([(k, 0) for k in lvlip.RETIRED_KERNELS] +
+                 [(lvlip.KERNEL_WAVE, 2), (lvlip.KERNEL_WFLAT, 0), (lvlip.KERNEL_FLAT, 6),
+                  (lvlip.KERNEL_FLAT, 4 | (2 << 8)), (lvlip.KERNEL_FLAT_OCC, 8 | (6 << 8))]):
         cfg = lvlip.LaunchCfg(k, u, 0, 0)
         assert L.lvlip_csum_batch_dev_ex(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(), None,
                                          ctypes.byref(cfg)) == lvlip.EINVAL, (k, u)
-    for k in (6, 7):
+    for k in lvlip.RETIRED_KERNELS:
         cfg = lvlip.LaunchCfg(k, 0, 0, 0)
         assert lvlip.lab().lvlip_lab_batch_dev_ex(base.data_ptr(), descs.data_ptr(), 1, out.data_ptr(),
                                                   None, ctypes.byref(cfg)) == lvlip.EINVAL, k
@@ -899,8 +815,6 @@ def test_max_int_packet():
     for variant in [(lvlip.KERNEL_AUTO, 0, 0), (lvlip.KERNEL_WAVE, 2, 0), (lvlip.KERNEL_FLAT, 0, 0),
                     (lvlip.KERNEL_FLAT, 4 | (2 << 8), 0), (lvlip.KERNEL_WINDOW, 2 | (3 << 8), 0),
                     (lvlip.KERNEL_WINDOW, 3 | (1 << 8), 1), (lvlip.KERNEL_WFLAT, 0, 0),
-                    (lvlip.KERNEL_RFLAT, 0, 0), (lvlip.KERNEL_WSFLAT, 0, 0),
-                    (lvlip.KERNEL_WAVE_SIMPLE, 2, 0), (lvlip.KERNEL_WAVE_LDS, 2, 0),
                     (lvlip.KERNEL_LANE, 0, 0), (lvlip.KERNEL_LANE, 2 | (4 << 8) | (1 << 16), 0)]:
         assert list(run(base, descs, variant)) == list(want), variant
     # AUTO with the caller's hint (the batch's average length: k_window, G 3)

@@ -170,16 +170,20 @@ def test_tx_checksum_dev_matches_reference_tx():
 
 
 def test_tx_checksum_dev_plain_and_nt_stores_agree():
-    """The device TX fill with both field-store kinds (nontemporal, the product;
-    plain stores, the lab variant) and the lab's other shapes (8 loads per
-    round, block order): identical frames, equal to the oracle's fill, odd and
-    even field addresses (frames at every alignment)."""
+    """The device TX fill with every field-store kind (the product's `nt sc0
+    sc1`; the lab's nontemporal, plain, sc0, sc1, sc0 sc1, nt sc1 and whole
+    32-B / 64-B blocks) and the lab's other shapes (8 loads per round, block
+    order): identical frames, equal to the oracle's fill, odd and even field
+    addresses (frames at every alignment)."""
     fr = workloads.frames(3000, seed=58) + workloads.frames(100, seed=59, max_l4=8900)
     want = [bytearray(f) for f in fr]
     for f in want:
         skb_oracle.tx_fill(f)
     buf, fd = lvlip.pack_frames(fr, align_mod=16, seed=5)
-    for kind in ("nt", "plain", 2, 4, 7):
+    # product (nt sc0 sc1 field stores), then the lab's: plain, 8 loads per
+    # round, block order, U 8 blocks plain, whole 32-B / 64-B blocks, and the
+    # field stores' cache policies sc0 .. nt sc0 sc1 (round 4)
+    for kind in ("nt", "plain", 2, 4, 6, 7, 16, 32, 64, 128, 192, 256, 320):
         base = _dev(buf)
         if kind == "nt":
             st = lvlip.tx_checksum_dev(base, fd)
@@ -351,10 +355,10 @@ def _echo_requests(rng, n, ihl_max=5):
     return out, kinds
 
 
-def _run_echo_dev(frames):
+def _run_echo_dev(frames, flags=0):
     buf, fd = lvlip.pack_frames(frames, align_mod=16, seed=9)
     base = _dev(buf)
-    st = lvlip.icmp_echo_reply_dev(base, fd).cpu().numpy()
+    st = lvlip.icmp_echo_reply_dev(base, fd, flags=flags).cpu().numpy()
     out = base.cpu().numpy()
     got = [out[int(d["offset"]):int(d["offset"]) + int(d["len"])].tobytes() for d in fd]
     rest = np.ones(buf.size, dtype=bool)
@@ -427,3 +431,141 @@ def test_icmp_echo_reply_dev_agrees_with_reference_stack():
         n = int.from_bytes(g[16:18], "big") - 20
         assert g[34:34 + n] == r[34:34 + n], (i, kinds[i])
     assert {"ffff", "zero", "ones"} <= set(kinds)
+
+
+def _corrupt_icmp(frames, rng):
+    """Echo requests whose ICMP checksum field no longer verifies."""
+    out = []
+    for f in frames:
+        g = bytearray(f)
+        l4 = 14 + (g[14] & 0xF) * 4
+        old = bytes(g[l4 + 2:l4 + 4])
+        while bytes(g[l4 + 2:l4 + 4]) == old or g[l4 + 2:l4 + 4] in (b"\x00\x00", b"\xff\xff"):
+            g[l4 + 2:l4 + 4] = rng.integers(0, 256, 2, dtype=np.uint8).tobytes()
+        out.append(g)
+    return out
+
+
+def test_icmp_echo_reply_dev_corrupted_requests_pin_both_modes():
+    """a request whose ICMP checksum does not verify.  level-ip
+    answers it with icmpv4_reply's full recomputation (src/icmpv4.c:11 never
+    verifies, :45-47 recompute).  flags 0 (the documented precondition is
+    broken): the lane writes the RFC 1624 field from the request's field, which
+    differs from the reference's for these frames, status 1.  LVLIP_ECHO_FULL:
+    the reference's bytes for every frame, status 2."""
+    rng = np.random.default_rng(74)
+    good, _ = _echo_requests(rng, 3000, ihl_max=15)
+    bad = _corrupt_icmp(good, rng)
+    st0, got0 = _run_echo_dev(bad)
+    stf, gotf = _run_echo_dev(bad, flags=lvlip.ECHO_FULL)
+    differ = 0
+    for f, g0, gf, s0 in zip(bad, got0, gotf, st0):
+        ref = _icmp_reply_ref(f)
+        assert gf == ref
+        l4 = 14 + (f[14] & 0xF) * 4
+        hc = int.from_bytes(f[l4 + 2:l4 + 4], "little")
+        inc = lvlip.icmp_echo_reply_csum(hc)
+        if inc != lvlip.CSUM_RECOMPUTE:
+            assert s0 == 1 and int.from_bytes(g0[l4 + 2:l4 + 4], "little") == inc
+            assert g0[l4] == 0 and g0[:l4 + 2] == ref[:l4 + 2] and g0[l4 + 4:] == ref[l4 + 4:]
+        differ += g0 != ref
+    assert (stf == 2).all()
+    assert differ > 2900  # the incremental field is wrong for (almost) every corrupted request
+
+
+def test_icmp_echo_reply_dev_full_equals_oracle():
+    """LVLIP_ECHO_FULL on the verified requests of the corner-case test (ihl
+    5-15, 0xffff fields, both undecidable kinds) and on non-requests: every
+    frame equals the oracle's icmpv4_reply recomputation, non-requests stay
+    untouched (status 0)."""
+    rng = np.random.default_rng(75)
+    fr, kinds = _echo_requests(rng, 8000, ihl_max=15)
+    others = workloads.frames(300, seed=76)
+    for f in others:
+        if f[23] == 1:
+            f[14 + (f[14] & 0xF) * 4] = int(rng.choice([0, 3, 11]))
+    st, got = _run_echo_dev(fr + others, flags=lvlip.ECHO_FULL)
+    for i, (f, g) in enumerate(zip(fr, got)):
+        assert g == _icmp_reply_ref(f), (i, kinds[i])
+    assert (st[:len(fr)] == 2).all()
+    for f, g, s in zip(others, got[len(fr):], st[len(fr):]):
+        assert s == 0 and g == bytes(f)
+
+
+@pytest.mark.skipif(not os.path.exists(ref_rx_cases.REF_SO), reason="oracle/_ref/libref.so not built")
+def test_icmp_echo_reply_dev_full_agrees_with_reference_stack_on_corrupted():
+    """Corrupted requests (the ICMP field garbage) through level-ip's own ip_rcv
+    -> icmpv4_reply (oracle/_ref/libref.so), which answers them: the
+    LVLIP_ECHO_FULL reply's ICMP part equals the stack's for every one."""
+    rng = np.random.default_rng(77)
+    fr, _ = _echo_requests(rng, 1000)
+    fr = _corrupt_icmp(fr, rng)
+    for f in fr:
+        f[14 + 12:14 + 16] = bytes([10, 0, 0, 5])
+        f[14 + 16:14 + 20] = bytes([10, 0, 0, 4])
+        f[14 + 6:14 + 8] = b"\x40\x00"
+        f[14 + 10:14 + 12] = b"\x00\x00"
+        c = lvlip.checksum(bytes(f[14:34]), 20, 0)
+        f[24:26] = c.to_bytes(2, "little")
+        f[0:6] = bytes.fromhex("000c296d5025")
+    replies = ref_rx_cases.reference_replies(fr)
+    assert all(r is not None for r in replies)
+    _, got = _run_echo_dev(fr, flags=lvlip.ECHO_FULL)
+    for i, (g, r) in enumerate(zip(got, replies)):
+        n = int.from_bytes(g[16:18], "big") - 20
+        assert g[34:34 + n] == r[34:34 + n], i
+
+
+def _tx_kinds():
+    return [None, 7, 16, 32, 128, 320]
+
+
+def test_tx_fill_dev_block_stores_every_alignment_and_packed_frames():
+    """VERDICT r03 Next #1's cases for the whole-block field stores (lab
+    variants 16 / 32) and the product: frames starting at every offset mod 32
+    (and mod 64), 54-B TCP frames (14 + 20 + 20: both fields inside one 32-B
+    sector for some offsets, the next frame's first bytes in the same block)
+    packed back to back with no gap, and ICMP frames whose two fields share a
+    sector.  Every variant's frames equal the oracle's fill, and no byte
+    outside the frames changes."""
+    rng = np.random.default_rng(90)
+    fr = []
+    for k in range(64 * 6):
+        f = workloads.frames(1, seed=1000 + k, max_l4=int(rng.choice([20, 24, 40, 200])),
+                             options=bool(k % 3 == 0), protos=(6,) if k % 2 else (1,))[0]
+        fr.append(f)
+    # 54-B TCP frames (no options, 20-B segment), packed back to back
+    tight = workloads.frames(256, seed=91, max_l4=20, options=False, protos=(6,))
+    for f in tight:
+        del f[14 + 20 + 20:]
+        f[16:18] = (40).to_bytes(2, "big")
+    want = [bytearray(f) for f in fr + tight]
+    for f in want:
+        skb_oracle.tx_fill(f)
+    # every frame of `fr` at its own offset mod 64: a 64-B aligned slot plus k
+    slots, off = [], 0
+    for k, f in enumerate(fr):
+        off = (off + 63) // 64 * 64 + (k % 64)
+        slots.append(off)
+        off += len(f)
+    for f in tight:  # back to back, from an odd offset
+        slots.append(off + 1 if f is tight[0] else off)
+        off = slots[-1] + len(f)
+    buf = rng.integers(0, 256, (off + 64 + 15) // 16 * 16, dtype=np.uint8)
+    allf = fr + tight
+    for o, f in zip(slots, allf):
+        buf[o:o + len(f)] = np.frombuffer(bytes(f), np.uint8)
+    fd = np.zeros(len(allf), dtype=lvlip.FRAME_DESC_DTYPE)
+    fd["offset"] = slots
+    fd["len"] = [len(f) for f in allf]
+    outside = np.ones(buf.size, bool)
+    for o, f in zip(slots, allf):
+        outside[o:o + len(f)] = False
+    for kind in _tx_kinds():
+        base = _dev(buf)
+        st = lvlip.tx_checksum_dev(base, fd) if kind is None else lvlip.frames_variant_dev(0, kind, base, fd)
+        assert int(st.sum()) == len(allf), kind
+        out = base.cpu().numpy()
+        got = [out[o:o + len(f)].tobytes() for o, f in zip(slots, allf)]
+        assert got == [bytes(f) for f in want], kind
+        assert np.array_equal(out[outside], buf[outside]), kind
