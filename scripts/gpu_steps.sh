@@ -40,7 +40,7 @@ for step in "$@"; do
     bench:*) wl=${step#bench:}; run "bench_$wl" 300 python bench.py --workload "$wl" ;;
     txstore) run txstore 400 python scripts/lab_tx_store.py "gpurun_out/${TAG}_tx_store.json" 7 ;;
     txpmc)
-      for v in ${TXPMC_VARIANTS:-tx_product tx_plain rx_l4}; do
+      for v in ${TXPMC_VARIANTS:-tx_product tx_nt tx_sec32 rx_l4}; do
         for c in FETCH_SIZE WRITE_SIZE; do
           run "txpmc_${v}_$c" 180 /opt/rocm/bin/rocprofv3 --pmc "$c" --kernel-include-regex "k_flat2|k_probe" \
             --output-format csv -d "gpurun_out/txpmc/${v}_$c" -o "${v}_$c" -- python3 scripts/lab_tx_store.py --only "$v" 20

@@ -7,7 +7,9 @@
 The mixed config's 2M frames made valid IPv4/TCP/ICMP frames in HBM (as
 bench.py --frames builds them).  Timed in interleaved rounds in one process,
 HIP events, 10 launches each:
-  tx_product     lvlip_tx_checksum_dev (k_flat2 U 8, 2-B nontemporal field stores)
+  tx_product     lvlip_tx_checksum_dev (k_flat2 U 8, 2-B field stores; `nt sc0
+                 sc1` since round 4)
+  tx_nt          the same with nontemporal 2-B stores (round 3's product; variant 6)
   tx_plain       the same with plain (temporal) 2-B field stores (variant 7)
   tx_sec32       the same kernel writing the aligned 32-B sector around each
                  field whole (lab frames variant 16; 2-B stores where the sector
@@ -41,7 +43,7 @@ import workloads  # noqa: E402
 PROBES = {"st_2b": 0, "st_2b_rmw": 1, "st_sec32": 2, "st_sec32_noload": 3, "st_blk64": 4, "st_2b_plain": 5,
           "st_2b_sc0": 6, "st_2b_sc1": 7, "st_2b_sc0sc1": 8, "st_2b_ntsc1": 9, "st_2b_ntsc0sc1": 10}
 # TX fill variants of lvlip_lab_frames_dev mode 0 (the product's shape, U 8 blocks)
-TX_VARIANTS = {"tx_plain": 7, "tx_sec32": 16, "tx_sec64": 32, "tx_sc0": 64, "tx_sc1": 128, "tx_sc0sc1": 192,
+TX_VARIANTS = {"tx_nt": 6, "tx_plain": 7, "tx_sec32": 16, "tx_sec64": 32, "tx_sc0": 64, "tx_sc1": 128, "tx_sc0sc1": 192,
                "tx_ntsc1": 256, "tx_ntsc0sc1": 320}
 
 
