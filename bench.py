@@ -9,7 +9,10 @@ segments).  Prints ONE JSON line (rank 0):
   roofline    the checksum kernel's achieved algorithmic GB/s (HIP events on the launch
               stream) against the 8 TB/s HBM3E peak; frac_aggregate = value / (N x 8 TB/s);
               traffic = PMC-measured HBM bytes per launch from profiles/ when a matching
-              measurement is committed, else null
+              measurement is committed (traffic_source names the file: the builder's
+              box, not this run's), else null; achieved_contract / frac_contract
+              count SURVEY.md §8(d)'s algorithmic bytes exactly (the bytes summed +
+              2 B per result; achieved counts the summed bytes only, 0.13 % less)
   verified_bit_exact  every one of the N outputs of the timed batch, copied back from
               HBM after the timed loop, equals level-ip's own checksum() (oracle/_ref,
               compiled from src/utils.c) run over the same bytes; on every rank
@@ -106,9 +109,11 @@ KERNEL_FN = {"window": "k_window", "wave": "k_stream", "flat": "k_flat2", "wflat
 
 
 def traffic_from_profiles(workload: str, kernel_label: str, kernel_fn: str):
-    """HBM bytes per launch measured by rocprofv3 PMC (profiles/*pmc*.json, see
-    profiles/README.md) for this workload, launch label and device function (the
-    newest file wins), or None when no matching measurement is committed."""
+    """(HBM bytes per launch, file) measured by rocprofv3 PMC (profiles/*pmc*.json,
+    see profiles/README.md) for this workload, launch label and device function
+    (the newest file wins), or None when no matching measurement is committed.
+    The counters are the builder's box's, committed with the code: the bench
+    does not run a PMC pass itself (it would need rocprofv3 around it)."""
     pdir = os.path.join(ROOT, "profiles")
     best = None
     if not os.path.isdir(pdir):
@@ -129,7 +134,7 @@ def traffic_from_profiles(workload: str, kernel_label: str, kernel_fn: str):
                 continue
             if (r.get("workload") == workload and r.get("kernel") == kernel_label
                     and r.get("kernel_regex") == kernel_fn):
-                best = r.get("hbm_bytes_per_launch")
+                best = (r.get("hbm_bytes_per_launch"), f"profiles/{fn}")
     return best
 
 
@@ -529,6 +534,7 @@ def run(args, world: int):
     total_bytes = sum(r["bytes"] for r in per_rank)
     value = total_bytes * args.steps / wall_max / 1e9 if wall_max > 0 else 0.0
     achieved = b.algo_bytes / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0  # rank 0's kernel
+    achieved_c = (b.algo_bytes + 2 * b.n) / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
     rank_ach = [r["bytes"] / (r["kernel_ms"] / 1e3) / 1e9 if r["kernel_ms"] > 0 else 0.0 for r in per_rank]
     for r, info, a in zip(per_rank, ranks, rank_ach):
         info.update({"kernel_ms": round(r["kernel_ms"], 5), "kernel_GBps": round(a, 2),
@@ -568,6 +574,7 @@ def run(args, world: int):
         cpu = cpu_baseline(b, first_chunk, cpus)
 
     if rank == 0:
+        tr = traffic_from_profiles(args.workload, kernel_label, KERNEL_FN.get(chosen, ""))
         rec = {
             "metric": METRIC, "value": None if args.dry_run else round(value, 2), "unit": "GB/s",
             "n_gpus": world,
@@ -585,12 +592,18 @@ def run(args, world: int):
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "frac_aggregate": round(value / (world * HBM_PEAK_GBPS), 4),
                          "frac_min_rank": round(min(rank_ach) / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic_from_profiles(args.workload, kernel_label,
-                                                          KERNEL_FN.get(chosen, "")),
+                         "traffic": tr[0] if tr else None,
+                         "traffic_source": tr[1] if tr else None,
                          "kernel_ms": round(kern_ms, 5),
                          "launches_per_step": launches,
                          "kernel_ms_per_launch": round(kern_ms / launches, 5),
-                         "algo_bytes_per_launch": b.algo_bytes // launches},
+                         "algo_bytes_per_launch": b.algo_bytes // launches,
+                         # SURVEY.md §8(d)'s algorithmic bytes: the bytes summed
+                         # plus the 2-B results written (achieved above counts
+                         # the summed bytes only, 0.13 % less on tcp1500)
+                         "contract_bytes_per_launch": (b.algo_bytes + 2 * b.n) // launches,
+                         "achieved_contract": round(achieved_c, 2),
+                         "frac_contract": round(achieved_c / HBM_PEAK_GBPS, 4)},
             "cpu_baseline": cpu,
             "verified_bit_exact": verified,
             "dist": {"world_size": dist.get_world_size() if world > 1 else 1,

@@ -495,6 +495,55 @@ extern "C" int lvlip_lab_probe_fields(void* buf, const void* frames, uint32_t n,
     return -1;
 }
 
+// ---- address-class probe (round 4): is there XCD <-> memory locality? -------
+// The buffer is cut into units of CB bytes; unit u has class u mod 8 and is
+// read by the waves of block slot x = ((u mod 8) + shift) mod 8 (block b runs
+// on XCD b % 8, as observed).  Each block slot's units form its own stream,
+// dealt to its waves in 4 KiB chunks round robin (the window probe's best
+// shape), U 1-KiB loads in flight per wave.  If memory were interleaved over
+// the stacks at CB granularity by (address / CB) mod 8, and an XCD reached
+// some stacks faster than others, one shift would read faster than the rest.
+namespace {
+template <int U>
+__global__ __launch_bounds__(256) void k_probe_xcd(const uint4* __restrict__ src, uint64_t bytes, uint32_t cb_log2,
+                                                   uint32_t shift, uint32_t* __restrict__ sink) {
+    uint32_t acc = 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t slot = blockIdx.x & 7u;
+    const uint64_t nwx = (uint64_t)(gridDim.x >> 3) * 4u;  // waves per block slot
+    const uint64_t r = (uint64_t)(blockIdx.x >> 3) * 4u + wid;
+    const uint32_t cls = (slot + 8u - (shift & 7u)) & 7u;   // the class this slot reads
+    const uint64_t cb = 1ull << cb_log2;
+    const uint64_t units = bytes >> cb_log2;
+    const uint64_t per_slot = units / 8u;                   // whole rounds of 8 classes
+    const uint64_t stream = per_slot << cb_log2;            // bytes of this slot's stream
+    const uint64_t chunks = stream / 4096u;
+    for (uint64_t c = r; c < chunks; c += nwx) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t q = c * 4096u + (uint64_t)u * 1024u + lane * 16u;  // offset in the slot's stream
+            const uint64_t j = q >> cb_log2, off = q & (cb - 1u);
+            v[u] = ld<true>(src + (((j * 8u + cls) << cb_log2) + off) / 16u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += words(v[u]);
+    }
+    acc = wsum(acc);
+    if (lane == 0) atomicAdd(sink, acc);
+}
+}  // namespace
+
+// cb_log2: 8 (256 B) .. 21 (2 MiB); shift 0-7; blocks a multiple of 8.
+extern "C" int lvlip_lab_probe_xcd(const void* src, uint64_t bytes, uint32_t* sink, uint32_t cb_log2,
+                                   uint32_t shift, int blocks, void* stream) {
+    if (!src || !sink || cb_log2 < 8 || cb_log2 > 24 || (blocks & 7) || blocks <= 0) return -1;
+    hipLaunchKernelGGL(k_probe_xcd<4>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4*)src, bytes, cb_log2, shift, sink);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 // ---- cross-XCD atomicity probe -----------------------------------------------
 // Every wave's lane 0 takes K tickets from one counter: MODE 0 agent-scope
 // atomicAdd (global_atomic_add ... sc0), MODE 1 system scope (... sc0 sc1),

@@ -50,6 +50,15 @@ def check_line(line: dict, steps: int, warmup: int):
     assert line["value"] == pytest.approx(total / (line["ms_per_step"] * 1e-3) / 1e9,
                                           rel=5e-3)
     assert line["value"] <= r["achieved"] * 1.01
+    # SURVEY §8(d)'s figure beside it (round 4 on): summed bytes + 2 B per result
+    if "achieved_contract" in r:
+        n = line["config"]["descriptors_per_gpu"]
+        assert r["contract_bytes_per_launch"] == (line["config"]["bytes_per_gpu"] + 2 * n) // nl
+        assert r["achieved_contract"] == pytest.approx(
+            r["contract_bytes_per_launch"] / (r["kernel_ms_per_launch"] * 1e-3) / 1e9, rel=2e-3)
+        assert r["frac_contract"] == pytest.approx(r["achieved_contract"] / r["peak"], rel=2e-3)
+        assert r["achieved"] < r["achieved_contract"] < r["achieved"] * 1.01
+        assert (r["traffic"] is None) == (r["traffic_source"] is None)
 
 
 # committed line -> (algorithmic bytes per launch, bound on PMC traffic / algorithmic)
@@ -72,7 +81,7 @@ def test_profile_scan_reads_every_committed_pmc_file():
 
     for wl, fn in (("tcp1500", "k_window"), ("tcp9000", "k_window"), ("mixed", "k_flat2")):
         t = bench.traffic_from_profiles(wl, "auto-u0-w0", fn)
-        assert t is not None and t > 0, wl
+        assert t is not None and t[0] > 0 and os.path.exists(os.path.join(ROOT, t[1])), wl
     assert bench.traffic_from_profiles("hdr20", "auto-u0-w0", "k_lane") is None
 
 
