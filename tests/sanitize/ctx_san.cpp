@@ -171,6 +171,38 @@ int main() {
     CHECK(lvlip_csum_ctx_destroy(ctx) == LVLIP_OK, "destroy");
     free(left);
 
+    // Group 4: one batch over three contexts, a host thread each
+    // (lvlip_csum_batch_host_flat_multi; every part's span gathered from one
+    // buffer that ends at its last packet's last byte)
+    {
+        Rng r{300};
+        const uint32_t n = 30000;
+        std::vector<lvlip_csum_desc> d(n);
+        uint64_t off = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            off += r() % 24u;
+            d[i].offset = off;
+            d[i].len = (r() % 61u == 0) ? -(int32_t)(r() % 3u) : (int32_t)(r() % 1601u);
+            d[i].start_sum = r();
+            off += d[i].len > 0 ? (uint64_t)d[i].len : 0u;
+        }
+        const size_t bytes = off ? off : 1;
+        uint8_t* base = (uint8_t*)malloc(bytes);
+        for (size_t b = 0; b < bytes; ++b) base[b] = (uint8_t)r();
+        lvlip_csum_ctx* mc[3] = {nullptr, nullptr, nullptr};
+        for (auto& c : mc) CHECK(lvlip_csum_ctx_create(&c, 0, 1u << 20) == LVLIP_OK, "multi ctx");
+        std::vector<uint16_t> out(n, 0);
+        CHECK(lvlip_csum_batch_host_flat_multi(mc, 3, base, bytes, d.data(), n, out.data()) == LVLIP_OK,
+              "batch_host_flat_multi");
+        for (uint32_t i = 0; i < n; ++i)
+            CHECK(out[i] == oracle_checksum(base + d[i].offset, d[i].len, (int)d[i].start_sum), "multi %u", i);
+        uint32_t cuts[4];
+        CHECK(lvlip_partition_bytes(d.data(), n, 3, cuts) == LVLIP_OK && cuts[0] == 0 && cuts[3] == n,
+              "partition");
+        for (auto& c : mc) CHECK(lvlip_csum_ctx_destroy(c) == LVLIP_OK, "multi destroy");
+        free(base);
+    }
+
     // one context per thread, concurrently (src/main.c:83-89 threads)
     std::vector<std::thread> th;
     for (int t = 0; t < 4; ++t)

@@ -244,11 +244,58 @@ static void frames(void)
     free(v);
 }
 
+/* 4. lvlip_partition_bytes (Group 4) on exact-size descriptor arrays against
+ *    the definition: cut p is the first index whose byte prefix reaches
+ *    p * T / parts (T the total of max(len, 0)), by count when T is 0. */
+static void partition(void)
+{
+    for (int trial = 0; trial < 400; trial++) {
+        const uint32_t n = rnd() % 700, parts = 1 + rnd() % 12;
+        lvlip_csum_desc *d = malloc((n ? n : 1) * sizeof *d);
+        uint32_t *cuts = malloc((parts + 1) * sizeof *cuts);
+        unsigned __int128 total = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t k = rnd() % 10;
+            d[i].offset = 0;
+            d[i].len = k == 0 ? -(int32_t)(rnd() % 5) : k == 1 ? 0 : k == 2 ? 0x7fffffff : (int32_t)(rnd() % 9001);
+            d[i].start_sum = 0;
+            total += d[i].len > 0 ? (uint32_t)d[i].len : 0u;
+        }
+        CHECK(lvlip_partition_bytes(n ? d : NULL, n, parts, cuts) == LVLIP_OK, "partition rc");
+        CHECK(cuts[0] == 0 && cuts[parts] == n, "partition ends");
+        for (uint32_t p = 1; p < parts; p++) {
+            uint32_t want = n;
+            if (n == 0)
+                want = 0;
+            else if (total == 0)
+                want = (uint32_t)((uint64_t)n * p / parts);
+            else {
+                const unsigned __int128 t = total * p / parts;
+                unsigned __int128 pre = 0;
+                for (uint32_t i = 0; i <= n; i++) {
+                    if (pre >= t) {
+                        want = i;
+                        break;
+                    }
+                    if (i < n)
+                        pre += d[i].len > 0 ? (uint32_t)d[i].len : 0u;
+                }
+            }
+            CHECK(cuts[p] == want, "partition trial %d n %u parts %u cut %u: %u != %u", trial, n, parts, p,
+                  cuts[p], want);
+        }
+        free(d);
+        free(cuts);
+    }
+    CHECK(lvlip_partition_bytes(NULL, 3, 2, NULL) == LVLIP_EINVAL, "partition NULL");
+}
+
 int main(void)
 {
     sweep();
     threads();
     frames();
+    partition();
     if (g_fail) {
         fprintf(stderr, "%d failures\n", g_fail);
         return 1;
