@@ -597,6 +597,35 @@ def test_host_iov_ragged_unaligned():
         assert list(ctx.batch_host(pkts, starts)) == want
 
 
+def test_host_flat_multi_contexts():
+    """Group 4: lvlip_csum_batch_host_flat_multi over 1, 3
+    and 8 contexts on device 0 (a thread each; on an 8-GPU node they would be
+    devices 0-7), against the oracle, on the mixed config's ragged frames and
+    on one context per part of lvlip_partition_bytes; a part's error comes
+    back (a context whose arena cannot hold one part's packet: LVLIP_ERANGE)."""
+    b = workloads.make("mixed", n=40000)
+    host = b.host_bytes()
+    want = pyoracle.batch(host, b.descs, threads=THREADS)
+    for k in (1, 3, 8):
+        ctxs = [lvlip.Context(0, arena_bytes=(1 << 20) if i % 2 else 0) for i in range(k)]
+        try:
+            assert np.array_equal(lvlip.batch_host_flat_multi(ctxs, host, b.descs), want), k
+        finally:
+            for c in ctxs:
+                c.close()
+    # one big packet in the last part, a 64 KiB arena there: that part fails
+    d = b.descs.copy()
+    d[-1]["offset"], d[-1]["len"] = 0, 200_000
+    ctxs = [lvlip.Context(0), lvlip.Context(0, arena_bytes=64 << 10)]
+    try:
+        with pytest.raises(lvlip.LvlipError) as e:
+            lvlip.batch_host_flat_multi(ctxs, host, d)
+        assert e.value.rc == lvlip.ERANGE
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 def test_host_flat_config_slices():
     b = workloads.make("mixed", n=30000)
     host = b.host_bytes()
