@@ -131,9 +131,10 @@ int lvlip_csum_batch_dev(const void *base, const lvlip_csum_desc *descs,
 /* Kernel selection for lvlip_csum_batch_dev_ex.  AUTO picks by len_hint:
  * >= 896 B -> WINDOW (shape by the hint); 1-32 B -> LANE; otherwise or
  * unknown -> FLAT (measured: DESIGN.md §4-5).  lvlip_auto_kernel() tells
- * which kernel and shape AUTO runs.  Ids 1, 2, 4, 5, 6, 7, 9, 11-13 are the A/B
- * variants measured against these (liblvlip_lab.so, not this library): here
- * they return LVLIP_EINVAL. */
+ * which kernel and shape AUTO runs.  Ids 1, 9 and 13 are A/B variants
+ * measured against these (liblvlip_lab.so, not this library), and 2, 4-7,
+ * 11, 12, 14 and 15 are retired: here all of them return
+ * LVLIP_EINVAL. */
 #define LVLIP_KERNEL_AUTO        0  /* the default                                 */
 #define LVLIP_KERNEL_FLAT        3  /* chunk-balanced tile sweep (ragged batches)  */
 #define LVLIP_KERNEL_WINDOW      8  /* one wavefront per packet, persistent, packets
@@ -255,8 +256,10 @@ int lvlip_partition_bytes(const lvlip_csum_desc *d, uint32_t n, uint32_t parts,
  * on a host thread of its own (its gather, copies and kernel overlap with the
  * other devices').  Waits for all parts; out[] is in descriptor order.  The
  * contexts are used by this call's threads only while it runs (the caller
- * must not use them concurrently).  Returns 0 or the first part's LVLIP_E*
- * in part order (results of failed parts are not meaningful). */
+ * must not use them concurrently), and must be distinct (a context is owned
+ * by one thread at a time: the same pointer twice is LVLIP_EINVAL).  Returns
+ * 0 or the first part's LVLIP_E* in part order (results of failed parts are
+ * not meaningful). */
 int lvlip_csum_batch_host_flat_multi(lvlip_csum_ctx *const *ctxs, uint32_t nctx,
                                      const void *base, size_t base_bytes,
                                      const lvlip_csum_desc *d, uint32_t n,

@@ -497,8 +497,11 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
 int lvlip_csum_batch_host_flat_multi(lvlip_csum_ctx* const* ctxs, uint32_t nctx, const void* base,
                                      size_t base_bytes, const lvlip_csum_desc* d, uint32_t n, uint16_t* out) {
     if (!ctxs || nctx == 0 || (n && (!base || !d || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
-    for (uint32_t k = 0; k < nctx; ++k)
+    for (uint32_t k = 0; k < nctx; ++k) {
         if (!ctxs[k]) return LVLIP_EINVAL;
+        for (uint32_t j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k]) return LVLIP_EINVAL;  // one thread per context
+    }
     if (n == 0) return LVLIP_OK;
     std::vector<uint32_t> cuts(nctx + 1u);
     int rc = lvlip_partition_bytes(d, n, nctx, cuts.data());

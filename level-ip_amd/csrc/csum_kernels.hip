@@ -19,9 +19,10 @@
 //   k_rx_hdr  : the header-only RX frame call, one lane per frame (csum_dev.h).
 //   k_echo_reply : f4, the RFC 1624 echo reply of verified requests (or, with
 //               LVLIP_ECHO_FULL, icmpv4_reply's full sum), one lane per frame.
-// The A/B variants measured against these (k_stream, k_wflat, k_rflat,
-// k_wsflat, the round-1 kernels, k_flat2's other shapes) live in
-// liblvlip_lab.so (lab_kernels.hip).
+// The A/B variants still under study (k_stream, k_wflat, k_flat2's other
+// shapes and occupancies, the frame calls' store forms) live in
+// liblvlip_lab.so (lab_kernels.hip); the ones rejected by >= 3 % were pruned
+// in round 4.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>

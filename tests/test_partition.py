@@ -74,3 +74,6 @@ def test_bad_arguments():
     assert L.lvlip_csum_batch_host_flat_multi(arr, 2, base.ctypes.data, 64, d.ctypes.data, 3,
                                               out.ctypes.data) == lvlip.EINVAL  # NULL contexts
     assert L.lvlip_icmp_echo_reply_dev_ex(None, None, 0, 2, None, None) == lvlip.EINVAL  # unknown flag
+    same = (ctypes.c_void_p * 2)(0x1000, 0x1000)  # one context twice: refused before it is touched
+    assert L.lvlip_csum_batch_host_flat_multi(same, 2, base.ctypes.data, 64, d.ctypes.data, 3,
+                                              out.ctypes.data) == lvlip.EINVAL
