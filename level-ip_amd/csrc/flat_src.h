@@ -329,15 +329,22 @@ struct FrameSrc {
         d0 = fr_mk(fd.offset + FR_ETH, ihl * 4u, 0u - x.le16(24));  // src/ip_output.c:42,53
         w |= 1u;
         if constexpr (SEC > 0) {
-            // which fields' SEC-byte blocks lie wholly inside [frame, frame + len)
+            // which fields' SEC-byte blocks lie wholly inside [frame, frame + len).
+            // A field at the last byte of a block straddles two blocks: then
+            // neither field of the frame is block-stored (a whole-block
+            // rewrite must never hold a byte another lane stores separately).
             const uint64_t fs = reinterpret_cast<uint64_t>(h), fe = fs + fd.len;
             const uint64_t fh = fs + FR_ETH + 10u, bh = fh & ~(uint64_t)(SEC - 1);
-            if (bh >= fs && bh + SEC <= fe) w |= FR_SEC_HDR;
-            if (w & FR_HAS_L4) {
-                const uint64_t fl = fs + l4 + ((w >> 16) & 0xffu), bl = fl & ~(uint64_t)(SEC - 1);
-                if (bl >= fs && bl + SEC <= fe) w |= FR_SEC_L4;
-                if (bl == bh && (w & FR_SEC_HDR)) w |= FR_SEC_SHARED;
-                w |= (uint32_t)(fl - fh) << 24;  // <= 60 + 16 - 10
+            const bool has_l4 = (w & FR_HAS_L4) != 0u;
+            const uint64_t fl = fs + l4 + ((w >> 16) & 0xffu), bl = fl & ~(uint64_t)(SEC - 1);
+            const bool straddle = (fh & (SEC - 1)) == SEC - 1 || (has_l4 && (fl & (SEC - 1)) == SEC - 1);
+            if (!straddle) {
+                if (bh >= fs && bh + SEC <= fe) w |= FR_SEC_HDR;
+                if (has_l4) {
+                    if (bl >= fs && bl + SEC <= fe) w |= FR_SEC_L4;
+                    if (bl == bh && (w & FR_SEC_HDR)) w |= FR_SEC_SHARED;
+                    w |= (uint32_t)(fl - fh) << 24;  // <= 60 + 16 - 10
+                }
             }
         }
     }
