@@ -14,6 +14,7 @@
 #   txpmc                 FETCH_SIZE / WRITE_SIZE passes of the TX variants
 #   modes:K               K processes of scripts/lab_modes.py (mixed line modes)
 #   numa                  scripts/lab_numa.py (XCD <-> address-class locality probe)
+#   window:SET            scripts/lab_window.py with LAB_SET=SET (read-order probes)
 #   evidence:WL           scripts/evidence.sh for WL (bench + trace + PMC)
 #   ab:WL:VARIANTS        scripts/ab.py on WL with a variant list (AB_VARIANTS syntax, no ':' inside
 #                         a variant here: use AB_VARIANTS directly for those)
@@ -50,6 +51,7 @@ for step in "$@"; do
       run txtrace 180 /opt/rocm/bin/rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/txpmc/trace \
         -o trace -- python3 scripts/lab_tx_store.py --only tx_product 20 ;;
     numa) run numa 300 python scripts/lab_numa.py "gpurun_out/${TAG}_numa.json" ;;
+    window:*) set_=${step#window:}; run "window_$set_" 400 env LAB_SET="$set_" python scripts/lab_window.py "gpurun_out/${TAG}_window_$set_.json" ;;
     modes:*)
       k=${step#modes:}
       for i in $(seq 1 "$k"); do run "modes_p$i" 240 python scripts/lab_modes.py "gpurun_out/${TAG}_modes_p$i.json"; done ;;

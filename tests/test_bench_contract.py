@@ -61,13 +61,14 @@ def check_line(line: dict, steps: int, warmup: int):
         assert (r["traffic"] is None) == (r["traffic_source"] is None)
 
 
-# committed line -> (algorithmic bytes per launch, bound on PMC traffic / algorithmic)
-TAG = "r03"
-COMMITTED = {
-    f"{TAG}_bench_tcp1500.json": (TCP1500_BYTES, 1.05),
-    f"{TAG}_bench_tcp9000.json": (1_048_576 * 9000, 1.05),
-    f"{TAG}_bench_mixed.json": (1_639_948_630, 1.15),  # layout + descriptors, DESIGN.md §5
-}
+# workload -> (algorithmic bytes per step, bound on PMC traffic / algorithmic)
+ALGO = {"tcp1500": (TCP1500_BYTES, 1.05), "tcp9000": (1_048_576 * 9000, 1.05),
+        "mixed": (1_639_948_630, 1.15)}  # mixed: layout + descriptors, DESIGN.md §5
+# every committed evidence set (round tag, workload): the bench line, the
+# same command's trace and the traced line, and the PMC summary
+EVIDENCE = sorted((f[:3], f[len("r0x_bench_"):-len(".json")]) for f in os.listdir(PROF)
+                  if f.startswith("r0") and "_bench_" in f and f[len("r0x_bench_"):-len(".json")] in ALGO)
+COMMITTED = {f"{tag}_bench_{wl}.json": ALGO[wl] for tag, wl in EVIDENCE if tag >= "r03"}
 # the device function AUTO runs for each committed line (bench.py KERNEL_FN)
 DOMINANT = {"tcp1500": "k_window", "tcp9000": "k_window", "mixed": "k_flat2"}
 
@@ -97,8 +98,8 @@ def test_committed_bench_line_consistent(name):
     assert line["roofline"]["algo_bytes_per_launch"] == per
     # the PMC traffic is per launch and within a few % of the algorithmic bytes
     # (committed beside the line; the line itself carries it once that file exists)
-    wl = name[len(f"{TAG}_bench_"):-len(".json")]
-    with open(os.path.join(PROF, f"{TAG}_pmc_{wl}.json")) as f:
+    tag, wl = name[:3], name[len("r0x_bench_"):-len(".json")]
+    with open(os.path.join(PROF, f"{tag}_pmc_{wl}.json")) as f:
         pmc = json.load(f)["kernels"][0]
     assert pmc["kernel_regex"] == DOMINANT[wl] and pmc["algo_bytes_per_launch"] == per
     assert 1.0 <= pmc["hbm_bytes_per_launch"] / per < max_ratio
@@ -119,18 +120,18 @@ def test_committed_bench_line_consistent(name):
     assert line["dist"]["world_size"] == 1 and line["roofline"]["frac_aggregate"] > 0
 
 
-@pytest.mark.parametrize("wl", sorted(DOMINANT))
-def test_committed_trace_matches_bench_line(wl):
+@pytest.mark.parametrize("tag,wl", [e for e in EVIDENCE if e[0] >= "r03"])
+def test_committed_trace_matches_bench_line(tag, wl):
     """The rocprofv3 kernel trace of the same command: its average launch
     agrees with the line the traced process printed (same process, 1 %), and
     with the committed un-profiled line within the process-to-process spread
     (the mixed line is bimodal across processes, 6.24 / 6.42
     TB/s, profiler or not; profiles/r03_mixed_spread/)."""
-    with open(os.path.join(PROF, f"{TAG}_bench_{wl}.json")) as f:
+    with open(os.path.join(PROF, f"{tag}_bench_{wl}.json")) as f:
         line = json.loads(f.read().strip().splitlines()[-1])
-    with open(os.path.join(PROF, f"{TAG}_{wl}_trace_line.json")) as f:
+    with open(os.path.join(PROF, f"{tag}_{wl}_trace_line.json")) as f:
         traced = json.loads(f.read().strip().splitlines()[-1])
-    with open(os.path.join(PROF, f"{TAG}_{wl}_kernel_stats.csv")) as f:
+    with open(os.path.join(PROF, f"{tag}_{wl}_kernel_stats.csv")) as f:
         rows = {r["Name"]: r for r in csv.DictReader(f)}
     ks = rows[DOMINANT[wl]]
     # the clock-settle steps (~1 000, their count varies with the run) + 50
