@@ -15,7 +15,8 @@
 #   modes:K               K processes of scripts/lab_modes.py (mixed line modes)
 #   numa                  scripts/lab_numa.py (XCD <-> address-class locality probe)
 #   window:SET            scripts/lab_window.py with LAB_SET=SET (read-order probes)
-#   evidence:WL           scripts/evidence.sh for WL (bench + trace + PMC)
+#   evidence:WL           scripts/evidence.sh for WL (bench + trace + PMC of the kernel AUTO runs)
+#   pmc:WL                the PMC passes of that evidence alone (scripts/profile.sh)
 #   ab:WL:VARIANTS        scripts/ab.py on WL with a variant list (AB_VARIANTS syntax, no ':' inside
 #                         a variant here: use AB_VARIANTS directly for those)
 set -u
@@ -55,7 +56,15 @@ for step in "$@"; do
     modes:*)
       k=${step#modes:}
       for i in $(seq 1 "$k"); do run "modes_p$i" 240 python scripts/lab_modes.py "gpurun_out/${TAG}_modes_p$i.json"; done ;;
-    evidence:*) wl=${step#evidence:}; run "evidence_$wl" 900 env TAG="$TAG" WL="$wl" bash scripts/evidence.sh ;;
+    evidence:*|pmc:*)
+      wl=${step#*:}
+      case "$wl" in mixed) kre=k_flat2 ;; *) kre=k_window ;; esac  # the kernel AUTO runs (bench.py KERNEL_FN)
+      if [ "${step%%:*}" = evidence ]; then
+        run "evidence_$wl" 900 env TAG="$TAG" WL="$wl" KRE="$kre" bash scripts/evidence.sh
+      else  # the PMC passes alone, into the same evidence directory
+        run "pmc_$wl" 600 env OUT="gpurun_out/evidence_${TAG}_$wl/prof" KRE="$kre" \
+          BENCH="bench.py --workload $wl --steps 20 --warmup 3 --settle-ms 0 --no-cpu-baseline" bash scripts/profile.sh
+      fi ;;
     ab:*) IFS=: read -r _ wl vars <<< "$step"
       run "ab_$wl" 600 env AB_WORKLOAD="$wl" AB_VARIANTS="$vars" python scripts/ab.py "gpurun_out/${TAG}_ab_$wl.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
