@@ -118,7 +118,10 @@ int main(int argc, char **argv)
     pthread_t th[MAX_CTX];
     for (uint32_t c = 0; c < k; c++) {
         parts[c] = (struct part){ctx[c], base, base_bytes, d + cuts[c], cuts[c + 1] - cuts[c], got2 + cuts[c], 0};
-        pthread_create(&th[c], NULL, run_part, &parts[c]);
+        if (pthread_create(&th[c], NULL, run_part, &parts[c]) != 0) {
+            fprintf(stderr, "multi_gpu: pthread_create failed for part %u\n", c);
+            return 1;
+        }
     }
     for (uint32_t c = 0; c < k; c++) {
         pthread_join(th[c], NULL);
