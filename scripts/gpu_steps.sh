@@ -10,6 +10,7 @@
 #   tests                 pytest -m gpu (one process, per-test timeout)
 #   smoke                 __graft_entry__.smoke()
 #   bench[:WL]            the default bench line (WL: tcp1500 | tcp9000 | mixed)
+#   frames                the mixed bench line with its device frame-call diag (TX fill, RX verify)
 #   txstore               scripts/lab_tx_store.py (TX field-store A/B + probes)
 #   txpmc                 FETCH_SIZE / WRITE_SIZE passes of the TX variants
 #   modes:K               K processes of scripts/lab_modes.py (mixed line modes)
@@ -41,6 +42,7 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 300 python bench.py ;;
     bench:*) wl=${step#bench:}; run "bench_$wl" 300 python bench.py --workload "$wl" ;;
+    frames) run frames 300 python bench.py --workload mixed --frames ;;
     txstore) run txstore 400 python scripts/lab_tx_store.py "gpurun_out/${TAG}_tx_store.json" 7 ;;
     txpmc)
       for v in ${TXPMC_VARIANTS:-tx_product tx_nt tx_sec32 rx_l4}; do
