@@ -424,6 +424,14 @@ extern "C" int lvlip_lab_probe_tl(const void* src, uint64_t bytes, uint32_t* sin
 //   4  the aligned 64-B blocks, loaded and stored back whole
 //   5  two 2-B plain (temporal) stores
 //   6-10  two 2-B stores with cache policy sc0 / sc1 / sc0 sc1 / nt sc1 / nt sc0 sc1
+//   11-16 (round 4, k_probe_sectors) the aligned B-byte block around each field
+//      written whole by B/16 adjacent lanes in ONE store instruction (one
+//      coalesced request per block, no load; once when both fields share it):
+//      11 B 32 nt, 12 B 32 plain, 13 B 64 nt, 14 B 64 plain, 15 B 32 nt sc0 sc1,
+//      16 B 128 plain; 17 / 18 B 64 loaded by the same four lanes first, then
+//      stored back nt / plain (the blocks' current bytes, as a TX fill must).  HBM3E has no write data mask, so a partial-sector write
+//      is a read-modify-write in the memory controller; a whole-sector request
+//      is not.
 namespace {
 typedef unsigned int pv4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) pv4 gpv4;
@@ -482,6 +490,29 @@ __global__ __launch_bounds__(256) void k_probe_fields(uint8_t* __restrict__ buf,
         if (s1 != s0) probe_block<NQ, MODE != 3>(s1, salt);
     }
 }
+
+// B/16 lanes per block, two blocks per frame: thread t -> frame t / (2 B/16),
+// field (t / (B/16)) & 1, quarter t % (B/16).
+template <int B, int POL>
+__global__ __launch_bounds__(256) void k_probe_sectors(uint8_t* __restrict__ buf, const uint4* __restrict__ fd,
+                                                       uint32_t n, uint32_t salt) {
+    constexpr uint32_t QB = B / 16, T = 2 * QB;
+    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t f = t / T;
+    if (f >= n) return;
+    const uint32_t r = (uint32_t)(t % T), field = r / QB, q = r % QB;
+    const uint4 d = fd[f];
+    const uint64_t fs = reinterpret_cast<uint64_t>(buf) + (((uint64_t)d.y << 32) | d.x);
+    const uint64_t s0 = (fs + 24u) & ~(uint64_t)(B - 1), s1 = (fs + 50u) & ~(uint64_t)(B - 1);
+    if (field == 1 && s1 == s0) return;
+    const uint64_t a = (field ? s1 : s0) + 16u * q;
+    pv4 v = pv4{salt ^ (uint32_t)f, salt, salt, salt};
+    if (POL >= 3) v = *reinterpret_cast<gpv4*>(a) ^ pv4{salt, salt, salt, salt};
+    if (POL == 0 || POL == 3) __builtin_nontemporal_store(v, reinterpret_cast<gpv4*>(a));
+    else if (POL == 4) *reinterpret_cast<gpv4*>(a) = v;
+    else if (POL == 1) *reinterpret_cast<gpv4*>(a) = v;
+    else asm volatile("global_store_dwordx4 %0, %1, off nt sc0 sc1" ::"v"(a), "v"(v) : "memory");
+}
 }  // namespace
 
 extern "C" int lvlip_lab_probe_fields(void* buf, const void* frames, uint32_t n, int mode, void* stream) {
@@ -492,6 +523,15 @@ extern "C" int lvlip_lab_probe_fields(void* buf, const void* frames, uint32_t n,
     if (mode == M) { hipLaunchKernelGGL(k_probe_fields<M>, g, b, 0, s, (uint8_t*)buf, (const uint4*)frames, n, 0u); return hipGetLastError() == hipSuccess ? 0 : -3; }
     PF(0) PF(1) PF(2) PF(3) PF(4) PF(5) PF(6) PF(7) PF(8) PF(9) PF(10)
 #undef PF
+#define PS(M, B, POL)                                                                                          \
+    if (mode == M) {                                                                                           \
+        const uint64_t th = (uint64_t)n * (2u * (B / 16u));                                                    \
+        hipLaunchKernelGGL((k_probe_sectors<B, POL>), dim3((uint32_t)((th + 255u) / 256u)), b, 0, s, (uint8_t*)buf, \
+                           (const uint4*)frames, n, 0u);                                                       \
+        return hipGetLastError() == hipSuccess ? 0 : -3;                                                       \
+    }
+    PS(11, 32, 0) PS(12, 32, 1) PS(13, 64, 0) PS(14, 64, 1) PS(15, 32, 2) PS(16, 128, 1) PS(17, 64, 3) PS(18, 64, 4)
+#undef PS
     return -1;
 }
 

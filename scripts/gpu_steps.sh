@@ -12,6 +12,7 @@
 #   bench[:WL]            the default bench line (WL: tcp1500 | tcp9000 | mixed)
 #   frames                the mixed bench line with its device frame-call diag (TX fill, RX verify)
 #   txstore               scripts/lab_tx_store.py (TX field-store A/B + probes)
+#   wb                    scripts/lab_wb.py (field-store forms paired with the RX + L4 sweep)
 #   txpmc                 FETCH_SIZE / WRITE_SIZE passes of the TX variants
 #   modes:K               K processes of scripts/lab_modes.py (mixed line modes)
 #   numa                  scripts/lab_numa.py (XCD <-> address-class locality probe)
@@ -43,6 +44,7 @@ for step in "$@"; do
     bench) run bench 300 python bench.py ;;
     bench:*) wl=${step#bench:}; run "bench_$wl" 300 python bench.py --workload "$wl" ;;
     frames) run frames 300 python bench.py --workload mixed --frames ;;
+    wb) run wb 400 python scripts/lab_wb.py "gpurun_out/${TAG}_wb.json" 5 ;;
     txstore) run txstore 400 python scripts/lab_tx_store.py "gpurun_out/${TAG}_tx_store.json" 7 ;;
     txpmc)
       for v in ${TXPMC_VARIANTS:-tx_product tx_nt tx_sec32 rx_l4}; do
