@@ -1185,10 +1185,10 @@ namespace lvlip {
 // frame source (flat_src.h) per at most kLaunchMax entries, whole frames per
 // launch.  Returns LVLIP_EHIP when a launch fails (the error stays readable by
 // hipGetLastError).
-template <int MODE, int U, int GORD, int PFA = 0, int SEC = 0, int STP = 0, int CB = 0>
+template <int MODE, int U, int GORD, int PFA = 0, int SEC = 0, int STP = 0>
 int launch_frames_flat(const void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* out8,
                        hipStream_t s, bool nt_store) {
-    using Src = FrameSrc<MODE, SEC, STP, CB>;
+    using Src = FrameSrc<MODE, SEC, STP>;
     const uint32_t per = lvlip_host::kLaunchMax / Src::SLOTS;
     for (uint32_t f0 = 0; f0 < n;) {
         const uint32_t m = n - f0 < per ? n - f0 : per;

@@ -244,19 +244,10 @@ __device__ __forceinline__ void fr_store16_pol(uint64_t a, uint32_t c) {
 // STP (TX): 0 = the launcher's nt_store flag (nontemporal or plain stores,
 // lab A/B); 2-6 = fr_store16_pol's cache policies; the product's TX fill
 // stores `nt sc0 sc1` (6).
-// CB (TX): 64 = the aligned 64-B block around a field, when it lies inside the
-// frame, is rewritten whole by four adjacent lanes in one store instruction
-// (put_blocks); fields outside such a block keep 2-B stores (STP's policy).
-template <int MODE, int SEC = 0, int STP = 0, int CB = 0>
+template <int MODE, int SEC = 0, int STP = 0>
 struct FrameSrc {
     static_assert(SEC == 0 || SEC == 32 || SEC == 64, "field block size");
     static_assert(STP == 0 || (STP >= 2 && STP <= 6), "field store policy");
-    // (lab diagnostics: CB 65 reloads the blocks but keeps 2-B field stores;
-    // CB 66 stores the blocks without the reload, zeros around the fields:
-    // wrong frame bytes, a timing probe on scratch frames only)
-    static_assert(CB == 0 || ((CB == 64 || CB == 65 || CB == 66) && SEC == 0 && MODE == FR_TX),
-                  "cooperative block size");
-    static constexpr uint32_t CBB = CB ? 64u : 0u;  // the block size
     const uint8_t* base;             // the frames' bytes
     uint8_t* wbase;                  // the same, writable (TX)
     const lvlip_frame_desc* frames;  // this launch's first frame
@@ -337,21 +328,20 @@ struct FrameSrc {
         }
         d0 = fr_mk(fd.offset + FR_ETH, ihl * 4u, 0u - x.le16(24));  // src/ip_output.c:42,53
         w |= 1u;
-        constexpr uint64_t SB = SEC > 0 ? SEC : CBB;
-        if constexpr (SB > 0) {
-            // which fields' SB-byte blocks lie wholly inside [frame, frame + len).
+        if constexpr (SEC > 0) {
+            // which fields' SEC-byte blocks lie wholly inside [frame, frame + len).
             // A field at the last byte of a block straddles two blocks: then
             // neither field of the frame is block-stored (a whole-block
             // rewrite must never hold a byte another lane stores separately).
             const uint64_t fs = reinterpret_cast<uint64_t>(h), fe = fs + fd.len;
-            const uint64_t fh = fs + FR_ETH + 10u, bh = fh & ~(SB - 1);
+            const uint64_t fh = fs + FR_ETH + 10u, bh = fh & ~(uint64_t)(SEC - 1);
             const bool has_l4 = (w & FR_HAS_L4) != 0u;
-            const uint64_t fl = fs + l4 + ((w >> 16) & 0xffu), bl = fl & ~(SB - 1);
-            const bool straddle = (fh & (SB - 1)) == SB - 1 || (has_l4 && (fl & (SB - 1)) == SB - 1);
+            const uint64_t fl = fs + l4 + ((w >> 16) & 0xffu), bl = fl & ~(uint64_t)(SEC - 1);
+            const bool straddle = (fh & (SEC - 1)) == SEC - 1 || (has_l4 && (fl & (SEC - 1)) == SEC - 1);
             if (!straddle) {
-                if (bh >= fs && bh + SB <= fe) w |= FR_SEC_HDR;
+                if (bh >= fs && bh + SEC <= fe) w |= FR_SEC_HDR;
                 if (has_l4) {
-                    if (bl >= fs && bl + SB <= fe) w |= FR_SEC_L4;
+                    if (bl >= fs && bl + SEC <= fe) w |= FR_SEC_L4;
                     if (bl == bh && (w & FR_SEC_HDR)) w |= FR_SEC_SHARED;
                     w |= (uint32_t)(fl - fh) << 24;  // <= 60 + 16 - 10
                 }
@@ -400,92 +390,9 @@ struct FrameSrc {
     // The field is addressed from the entry's own first byte (no second read of
     // the frame descriptor): L4 field at entry + (w >> 16), IPv4 header
     // checksum at entry + 10.
-    // CB: every lane computes its own block (the entry's field block, or the
-    // header lane's block both fields share), then the wave's owners (lane =
-    // entry) hand their blocks out in four rounds of 16, four lanes a block:
-    // each lane reloads its 16-B quarter (lines this workgroup's parse and
-    // sweep have just read), patches the field bytes it holds and stores it
-    // back nontemporally.  The four quarters go out in one store instruction,
-    // so the block reaches memory as one whole 64-B write where a 2-B field
-    // store is a partial write the memory side must read, merge and write
-    // back (HBM3E has no write data mask): 57 against 199 us for the mixed
-    // frames' fields beside the RX + L4 sweep (profiles/r04_wb.json).  All
-    // rounds' loads are issued before the first store (one round trip).
-    __device__ __forceinline__ void put_blocks(uint32_t i, uint16_t c, uint32_t w, bool valid,
-                                               uint64_t addr) const {
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        typedef __attribute__((address_space(1))) v4u gv4u;
-        constexpr uint32_t QB = CBB / 16, PER = 64 / QB;  // lanes per block, blocks per round
-        const uint32_t lane = threadIdx.x & 63u;
-        const uint32_t cl4 = (uint32_t)__shfl_xor((int)c, 1, 64) & 0xffffu;
-        const bool l4 = (i & 1u) != 0u;
-        uint64_t sa = 0;          // this lane's block (0: none)
-        uint32_t p0 = 0, p1 = 0;  // field patches: offset in the block | 0x8000 | value << 16
-        if (valid) {
-            if (!l4 && out8) out8[i / SLOTS] = (uint8_t)(w & 1u);
-            if ((w & 1u) && (!l4 || (w & FR_HAS_L4))) {
-                const uint64_t fa = addr + (l4 ? ((w >> 16) & 0xffu) : 10u);
-                if (CB == 65) fr_store16_pol<STP == 0 ? 6 : STP>(fa, c);
-                if (w & (l4 ? FR_SEC_L4 : FR_SEC_HDR)) {
-                    if (!(l4 && (w & FR_SEC_SHARED))) {  // else in the header lane's block
-                        sa = fa & ~(uint64_t)(CBB - 1);
-                        p0 = (uint32_t)(fa - sa) | 0x8000u | ((uint32_t)c << 16);
-                        if (!l4 && (w & FR_SEC_SHARED))
-                            p1 = ((uint32_t)(fa - sa) + (w >> 24)) | 0x8000u | (cl4 << 16);
-                    }
-                } else if (CB != 65) {
-                    fr_store16_pol<STP == 0 ? 6 : STP>(fa, c);
-                }
-            }
-        }
-        const uint64_t own = __ballot(sa != 0u);
-        const uint64_t safe = reinterpret_cast<uint64_t>(frames) & ~15ull;  // readable, never stored
-        const uint32_t qq = lane % QB;
-        v4u q[QB];
-        uint64_t ad[QB];
-        uint32_t pa[QB], pb[QB];
-#pragma unroll
-        for (uint32_t r = 0; r < QB; ++r) {
-            const int src = (int)(r * PER + lane / QB);
-            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)sa, src, 64);
-            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(sa >> 32), src, 64);
-            pa[r] = (uint32_t)__shfl((int)p0, src, 64);
-            pb[r] = (uint32_t)__shfl((int)p1, src, 64);
-            const uint64_t b = ((uint64_t)hi << 32) | lo;
-            ad[r] = b ? b + 16u * qq : 0u;
-            if (CB == 66)
-                q[r] = v4u{0u, 0u, 0u, 0u};
-            else
-                q[r] = *reinterpret_cast<const gv4u*>(ad[r] ? ad[r] : safe);
-        }
-        if (CB == 65) {  // the reloads alone: keep them, store nothing more
-#pragma unroll
-            for (uint32_t r = 0; r < QB; ++r) asm volatile("" ::"v"(q[r]));
-            return;
-        }
-#pragma unroll
-        for (uint32_t r = 0; r < QB; ++r) {
-            if (((own >> (r * PER)) & ((1ull << PER) - 1u)) == 0u) continue;  // wave-uniform
-            if (!ad[r]) continue;
-            uint32_t v[4] = {q[r].x, q[r].y, q[r].z, q[r].w};
-            const uint32_t pp[2] = {pa[r], pb[r]};
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                if (!(pp[k] & 0x8000u)) continue;
-                const int o = (int)(pp[k] & 0x7fffu) - 16 * (int)qq;
-                if (o >= -1 && o <= 15) fr_patch16<4>(v, (uint32_t)o, pp[k] >> 16);
-            }
-            __builtin_nontemporal_store(v4u{v[0], v[1], v[2], v[3]}, reinterpret_cast<gv4u*>(ad[r]));
-        }
-    }
-
     __device__ __forceinline__ void put(uint32_t i, uint16_t c, uint32_t w, bool valid,
                                         uint64_t addr) const {
         const uint32_t f = i / SLOTS;
-        if constexpr (CB > 0) {
-            put_blocks(i, c, w, valid, addr);
-            return;
-        }
         if (MODE == FR_TX) {
             // SEC: the header lane writes a block both fields share, so it
             // takes the L4 lane's result (every lane runs the shuffle)

@@ -710,14 +710,6 @@ __attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int va
             case 192: return lvlip::launch_frames_flat<lvlip::FR_TX, 8, 2, 0, 0, 4>(base, frames, n, out8, s, true);
             case 256: return lvlip::launch_frames_flat<lvlip::FR_TX, 8, 2, 0, 0, 5>(base, frames, n, out8, s, true);
             case 320: return lvlip::launch_frames_flat<lvlip::FR_TX, 8, 2, 0, 0, 6>(base, frames, n, out8, s, true);
-            // whole 64-B blocks by four lanes in one store (FrameSrc's CB), 2-B
-            // fields outside them `nt sc0 sc1`
-            case 512: return lvlip::launch_frames_flat<lvlip::FR_TX, 8, 2, 0, 0, 6, 64>(base, frames, n, out8, s, true);
-            // diagnostics of 512: the reloads alone (2-B stores kept), and the
-            // block stores without the reload (zeros around the fields: wrong
-            // frame bytes, scratch frames only)
-            case 576: return lvlip::launch_frames_flat<lvlip::FR_TX, 8, 2, 0, 0, 6, 65>(base, frames, n, out8, s, true);
-            case 640: return lvlip::launch_frames_flat<lvlip::FR_TX, 8, 2, 0, 0, 6, 66>(base, frames, n, out8, s, true);
             default: return LVLIP_EINVAL;
         }
     }

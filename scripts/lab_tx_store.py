@@ -17,14 +17,10 @@ HIP events, 10 launches each:
   tx_sec64       the same with 64-B blocks (variant 32)
   tx_sc0 .. tx_ntsc0sc1  2-B field stores with the cache-policy bits sc0, sc1,
                  sc0 sc1, nt sc1, nt sc0 sc1 (variants 64-320)
-  tx_cb64        the aligned 64-B block around each field rewritten whole by
-                 four lanes in one store instruction (variant 512; 2-B `nt sc0
-                 sc1` stores where the block leaves the frame)
-  tx_cb64_reload_only / tx_cb64_noreload  its two halves: the blocks' reloads
-                 with the product's 2-B stores (576), and the block stores
-                 without the reload (640: zeros around the fields, run on a
-                 fresh scratch copy of the frames per launch, not checked;
-                 compare with tx_product_copied, the product on the same copies)
+  (tx_cb64 / tx_cb64_reload_only / tx_cb64_noreload, whole 64-B blocks by
+                 four lanes in one store and its halves, variants 512 / 576 /
+                 640: measured in profiles/r04_tx_store_cb64.json, removed,
+                 last in commit fe59a5a)
   rx_l4          lvlip_rx_verify_dev with L4: the same sweep without stores
   st_*           lvlip_lab_probe_fields on a scratch copy of the buffer: the two
                  fields of every frame (+24, +50) stored alone, no sweep:
@@ -52,9 +48,10 @@ PROBES = {"st_2b": 0, "st_2b_rmw": 1, "st_sec32": 2, "st_sec32_noload": 3, "st_b
           "st_2b_sc0": 6, "st_2b_sc1": 7, "st_2b_sc0sc1": 8, "st_2b_ntsc1": 9, "st_2b_ntsc0sc1": 10}
 # TX fill variants of lvlip_lab_frames_dev mode 0 (the product's shape, U 8 blocks)
 TX_VARIANTS = {"tx_nt": 6, "tx_plain": 7, "tx_sec32": 16, "tx_sec64": 32, "tx_sc0": 64, "tx_sc1": 128, "tx_sc0sc1": 192,
-               "tx_ntsc1": 256, "tx_ntsc0sc1": 320, "tx_cb64": 512, "tx_cb64_reload_only": 576}
+               "tx_ntsc1": 256, "tx_ntsc0sc1": 320}
 # timing probes that write wrong frame bytes: run on a scratch copy, not checked
-TX_SCRATCH = {"tx_cb64_noreload": 640}
+# (round 4's tx_cb64_noreload, variant 640, until commit fe59a5a)
+TX_SCRATCH = {}
 
 
 def timed(fn, stream, reps=10, warm=2):
@@ -108,8 +105,10 @@ def main():
         calls[k] = (lambda vv: lambda: lvlip.frames_variant_dev(0, vv, base, fdt, stream=s))(v)
     # each launch on a fresh copy of the frames (the variant destroys them),
     # beside the product on a fresh copy: compare the two, not the others
-    scratch_tx = base.clone()
-    calls["tx_product_copied"] = lambda: (scratch_tx.copy_(base), lvlip.tx_checksum_dev(scratch_tx, fdt, stream=s))
+    scratch_tx = base.clone() if TX_SCRATCH else None
+    if TX_SCRATCH:
+        calls["tx_product_copied"] = lambda: (scratch_tx.copy_(base),
+                                              lvlip.tx_checksum_dev(scratch_tx, fdt, stream=s))
     for k, v in TX_SCRATCH.items():
         calls[k] = (lambda vv: lambda: (scratch_tx.copy_(base),
                                         lvlip.frames_variant_dev(0, vv, scratch_tx, fdt, stream=s)))(v)

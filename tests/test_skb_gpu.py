@@ -182,9 +182,8 @@ def test_tx_checksum_dev_plain_and_nt_stores_agree():
     buf, fd = lvlip.pack_frames(fr, align_mod=16, seed=5)
     # product (nt sc0 sc1 field stores), then the lab's: plain, 8 loads per
     # round, block order, U 8 blocks plain, whole 32-B / 64-B blocks, and the
-    # field stores' cache policies sc0 .. nt sc0 sc1, whole 64-B blocks by
-    # four lanes in one store (round 4)
-    for kind in ("nt", "plain", 2, 4, 6, 7, 16, 32, 64, 128, 192, 256, 320, 512):
+    # field stores' cache policies sc0 .. nt sc0 sc1 (round 4)
+    for kind in ("nt", "plain", 2, 4, 6, 7, 16, 32, 64, 128, 192, 256, 320):
         base = _dev(buf)
         if kind == "nt":
             st = lvlip.tx_checksum_dev(base, fd)
@@ -518,12 +517,12 @@ def test_icmp_echo_reply_dev_full_agrees_with_reference_stack_on_corrupted():
 
 
 def _tx_kinds():
-    return [None, 7, 16, 32, 128, 320, 512]
+    return [None, 7, 16, 32, 128, 320]
 
 
 def test_tx_fill_dev_block_stores_every_alignment_and_packed_frames():
     """VERDICT r03 Next #1's cases for the whole-block field stores (lab
-    variants 16 / 32 / 512) and the product: frames starting at every offset mod 32
+    variants 16 / 32) and the product: frames starting at every offset mod 32
     (and mod 64), 54-B TCP frames (14 + 20 + 20: both fields inside one 32-B
     sector for some offsets, the next frame's first bytes in the same block)
     packed back to back with no gap, and ICMP frames whose two fields share a
