@@ -335,7 +335,12 @@ int lvlip_csum_register(lvlip_csum_ctx* c, void* ptr, size_t bytes, uint32_t fla
     r.bytes = bytes;
     r.dev = (uint8_t*)dev;
     r.flags = flags;
-    c->regions.push_back(r);
+    try {  // no exception leaves the C ABI
+        c->regions.push_back(r);
+    } catch (...) {
+        (void)hipHostUnregister(ptr);
+        return LVLIP_ENOMEM;
+    }
     return LVLIP_OK;
 }
 
@@ -503,16 +508,22 @@ int lvlip_csum_batch_host_flat_multi(lvlip_csum_ctx* const* ctxs, uint32_t nctx,
             if (ctxs[j] == ctxs[k]) return LVLIP_EINVAL;  // one thread per context
     }
     if (n == 0) return LVLIP_OK;
-    std::vector<uint32_t> cuts(nctx + 1u);
+    std::vector<uint32_t> cuts;
+    std::vector<int> rcs;
+    std::vector<std::thread> th;
+    try {  // no exception leaves the C ABI
+        cuts.resize(nctx + 1u);
+        rcs.assign(nctx, LVLIP_OK);
+        th.reserve(nctx);
+    } catch (...) {
+        return LVLIP_ENOMEM;
+    }
     int rc = lvlip_partition_bytes(d, n, nctx, cuts.data());
     if (rc != LVLIP_OK) return rc;
-    std::vector<int> rcs(nctx, LVLIP_OK);
     auto part = [&](uint32_t k) {
         const uint32_t lo = cuts[k], hi = cuts[k + 1];
         if (hi > lo) rcs[k] = lvlip_csum_batch_host_flat(ctxs[k], base, base_bytes, d + lo, hi - lo, out + lo);
     };
-    std::vector<std::thread> th;
-    th.reserve(nctx);
     try {
         for (uint32_t k = 1; k < nctx; ++k) th.emplace_back(part, k);
     } catch (...) {
