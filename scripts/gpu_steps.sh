@@ -12,6 +12,7 @@
 #   bench[:WL]            the default bench line (WL: tcp1500 | tcp9000 | mixed)
 #   frames                the mixed bench line with its device frame-call diag (TX fill, RX verify)
 #   txstore               scripts/lab_tx_store.py (TX field-store A/B + probes)
+#   rehearse:N            bench.py --gpus N self-launched over gloo, the ranks sharing the one GPU
 #   wb                    scripts/lab_wb.py (field-store forms paired with the RX + L4 sweep)
 #   txpmc                 FETCH_SIZE / WRITE_SIZE passes of the TX variants
 #   modes:K               K processes of scripts/lab_modes.py (mixed line modes)
@@ -44,6 +45,7 @@ for step in "$@"; do
     bench) run bench 300 python bench.py ;;
     bench:*) wl=${step#bench:}; run "bench_$wl" 300 python bench.py --workload "$wl" ;;
     frames) run frames 300 python bench.py --workload mixed --frames ;;
+    rehearse:*) n=${step#rehearse:}; run "rehearse_n$n" 300 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --steps 50 --warmup 10 ;;
     wb) run wb 400 python scripts/lab_wb.py "gpurun_out/${TAG}_wb.json" 5 ;;
     txstore) run txstore 400 python scripts/lab_tx_store.py "gpurun_out/${TAG}_tx_store.json" 7 ;;
     txpmc)
