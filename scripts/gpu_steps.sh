@@ -10,6 +10,7 @@
 #   tests                 pytest -m gpu (one process, per-test timeout)
 #   smoke                 __graft_entry__.smoke()
 #   bench[:WL]            the default bench line (WL: tcp1500 | tcp9000 | mixed)
+#   e2e[:WL]              the bench line with its host-resident (PCIe-inclusive) rates and small-batch latency
 #   frames                the mixed bench line with its device frame-call diag (TX fill, RX verify)
 #   txstore               scripts/lab_tx_store.py (TX field-store A/B + probes)
 #   rehearse:N            bench.py --gpus N self-launched over gloo, the ranks sharing the one GPU
@@ -44,6 +45,8 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 300 python bench.py ;;
     bench:*) wl=${step#bench:}; run "bench_$wl" 300 python bench.py --workload "$wl" ;;
+    e2e) run e2e_tcp1500 300 python bench.py --e2e ;;
+    e2e:*) wl=${step#e2e:}; run "e2e_$wl" 300 python bench.py --workload "$wl" --e2e ;;
     frames) run frames 300 python bench.py --workload mixed --frames ;;
     rehearse:*) n=${step#rehearse:}; run "rehearse_n$n" 300 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --steps 50 --warmup 10 ;;
     wb) run wb 400 python scripts/lab_wb.py "gpurun_out/${TAG}_wb.json" 5 ;;
