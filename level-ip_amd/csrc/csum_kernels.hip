@@ -485,9 +485,9 @@ int dispatch_one(const void* base, const lvlip_csum_desc* descs, uint32_t n, uin
 }
 
 // The frame calls (include/lvlip_skb.h): the header-only RX call on k_rx_hdr,
-// TX fill and RX + L4 on k_flat2 with a frame source, 4 loads per round,
-// quarters order and nontemporal field stores (the measured
-// alternatives are lab variants).
+// TX fill and RX + L4 on k_flat2 with a frame source in block order (RX + L4
+// 4 loads per round; TX 8, its field stores `nt sc0 sc1`) (the
+// measured alternatives are lab variants).
 int launch_rx_hdr(const void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* out8,
                   hipStream_t s) {
     for (uint32_t f0 = 0; f0 < n;) {
