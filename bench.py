@@ -696,35 +696,102 @@ def frames_dev(lvlip, torch, dev):
     v = lvlip.rx_verify_dev(base, fdt, 0, stream=stream)
     torch.cuda.synchronize(dev)
     res["rx_header_all_ok"] = bool((v == lvlip.RX_OK).all())
-    # the same frames from host memory through the host API (PCIe-inclusive:
-    # plan on the CPU, gather, H2D, kernel, D2H, apply), on a 512K-frame prefix
-    import ctypes
-
+    # the same frames from host memory through the host API (PCIe-inclusive),
+    # on a 512K-frame prefix
     nh = min(n, 1 << 19)
     end = int(fd["offset"][nh - 1]) + int(fd["len"][nh - 1])
     host = base[: (end + 15) // 16 * 16].cpu().numpy().copy()
-    fr = np.zeros(nh, dtype=[("head", "<u8"), ("len", "<u4"), ("pad", "<u4")])
-    assert fr.dtype.itemsize == ctypes.sizeof(lvlip.Frame)
-    fr["head"] = host.ctypes.data + fd["offset"][:nh]
-    fr["len"] = fd["len"][:nh]
-    arr = ctypes.cast(fr.ctypes.data, ctypes.POINTER(lvlip.Frame))
-    verdict = np.zeros(nh, np.uint8)
-    hl4 = int(pay["len"][:nh].sum())
-    lib = lvlip.lib()
-    with lvlip.Context(dev.index or 0) as ctx:
-        for name, call, nbytes in (
-                ("host_tx_fill", lambda: lib.lvlip_tx_checksum(ctx._h, arr, nh), 20 * nh + hl4),
-                ("host_rx_header_l4", lambda: lib.lvlip_rx_verify(ctx._h, arr, nh, lvlip.RX_VERIFY_L4,
-                                                                 verdict.ctypes.data), 20 * nh + hl4)):
-            assert call() == 0, name
-            t0 = time.perf_counter()
-            for _ in range(3):
-                assert call() == 0, name
-            ms = (time.perf_counter() - t0) / 3 * 1e3
-            res[name] = {"frames": nh, "ms": round(ms, 3), "Mframes_per_s": round(nh / ms / 1e3, 2),
-                         "GBps": round(nbytes / ms / 1e6, 2)}
+    res["host"] = frames_host(lvlip, dev, host, fd[:nh], int(pay["len"][:nh].sum()))
     log("device-resident frames", res)
     return res
+
+
+def frames_host(lvlip, dev, host, fd, l4_bytes):
+    """The host frame calls (include/lvlip_skb.h lvlip_tx_checksum,
+    lvlip_rx_verify) on n frames in host memory, PCIe included, wall time per
+    call (1 warm-up, then the mean of 5), from each source the library knows
+    (frames_host.cpp):
+      slab       the frames in one pageable buffer, as laid out in HBM (the
+                 gather path: every frame one memcpy into the pinned arena)
+      scattered  every frame at the start of its own 1616-B slot (a malloc'd
+                 alloc_skb(BUFLEN) buffer, src/skbuff.c:5-20), the slots in
+                 random order over an n x 1616 B buffer (the gather path)
+      dma        the slab registered LVLIP_REG_DMA (copy engine reads spans)
+      zerocopy   the slab registered LVLIP_REG_ZEROCOPY (kernel reads in place)
+      hostplan   the slab through round 4's path (LVLIP_FRAME_PATH=hostplan:
+                 the CPU plans every frame, two gathered pieces per frame)
+    GB/s counts the checksummed bytes (20 B header + L4 per frame) as the
+    device lines do; frame_GBps counts the frames' bytes (what crosses PCIe)."""
+    import ctypes
+
+    n = fd.size
+    hb = 20 * n + l4_bytes
+    frame_bytes = int(fd["len"].sum())
+    stride = 1616
+    rng = np.random.default_rng(7)
+    slot = rng.permutation(n)
+    scat = np.zeros(n * stride, np.uint8)
+    for i in range(n):
+        o, ln = int(fd["offset"][i]), int(fd["len"][i])
+        scat[int(slot[i]) * stride:int(slot[i]) * stride + ln] = host[o:o + ln]
+
+    def frames_arr(buf, offsets):
+        fr = np.zeros(n, dtype=[("head", "<u8"), ("len", "<u4"), ("pad", "<u4")])
+        assert fr.dtype.itemsize == ctypes.sizeof(lvlip.Frame)
+        fr["head"] = buf.ctypes.data + offsets
+        fr["len"] = fd["len"]
+        return fr, ctypes.cast(fr.ctypes.data, ctypes.POINTER(lvlip.Frame))
+
+    lib = lvlip.lib()
+    verdict = np.zeros(n, np.uint8)
+    out = {"frames": n, "frame_bytes": frame_bytes, "checksummed_bytes": hb}
+
+    def run(ctx, arr, tag):
+        calls = (("tx_fill", lambda: lib.lvlip_tx_checksum(ctx._h, arr, n)),
+                 ("rx_header", lambda: lib.lvlip_rx_verify(ctx._h, arr, n, 0, verdict.ctypes.data)),
+                 ("rx_header_l4", lambda: lib.lvlip_rx_verify(ctx._h, arr, n, lvlip.RX_VERIFY_L4,
+                                                              verdict.ctypes.data)))
+        r = {}
+        for name, call in calls:
+            assert call() == 0, (tag, name)
+            if name == "rx_header":  # filled by tx_fill (L4: the lossy TCP seed may not verify)
+                assert (verdict == lvlip.RX_OK).all(), (tag, name)
+            t0 = time.perf_counter()
+            for _ in range(5):
+                assert call() == 0, (tag, name)
+            ms = (time.perf_counter() - t0) / 5 * 1e3
+            nb = 20 * n if name == "rx_header" else hb
+            r[name] = {"ms": round(ms, 3), "Mframes_per_s": round(n / ms / 1e3, 2),
+                       "GBps": round(nb / ms / 1e6, 2)}
+            if name != "rx_header":
+                r[name]["frame_GBps"] = round(frame_bytes / ms / 1e6, 2)
+        out[tag] = r
+        log(f"host frames {tag:9s}", {k: v["GBps"] for k, v in r.items()})
+
+    keep_slab = frames_arr(host, fd["offset"].astype(np.uint64))
+    keep_scat = frames_arr(scat, slot.astype(np.uint64) * stride)
+    d = dev.index or 0
+    with lvlip.Context(d) as ctx:
+        run(ctx, keep_slab[1], "slab")
+        run(ctx, keep_scat[1], "scattered")
+        for tag, flag in (("dma", lvlip.REG_DMA), ("zerocopy", lvlip.REG_ZEROCOPY)):
+            ctx.register(host, flag)
+            try:
+                run(ctx, keep_slab[1], tag)
+            finally:
+                ctx.unregister(host)
+    os.environ["LVLIP_FRAME_PATH"] = "hostplan"
+    try:
+        with lvlip.Context(d) as ctx:
+            run(ctx, keep_slab[1], "hostplan")
+    finally:
+        del os.environ["LVLIP_FRAME_PATH"]
+    # the frames the TX calls filled are what the HBM frames hold after
+    # tx_fill (same bytes, same fill): spot-check the slab against the scatter
+    for i in range(0, n, max(1, n // 997)):
+        o, ln = int(fd["offset"][i]), int(fd["len"][i])
+        assert np.array_equal(host[o:o + ln], scat[int(slot[i]) * stride:int(slot[i]) * stride + ln]), i
+    return out
 
 
 def read_probe(lvlip, torch, base, stream):

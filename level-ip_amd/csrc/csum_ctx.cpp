@@ -2,13 +2,8 @@
 //
 // level-ip's packets live in malloc'd skb heads (src/skbuff.c:5-20) at offsets
 // 14 (IPv4 header, include/ip.h:47-50) and 34 (TCP/ICMP, include/tcp.h:224-227),
-// i.e. 2 mod 4.  A context owns, per pipeline slot (two slots):
-//   - a pinned host arena the packets are gathered into, each at a 16-B
-//     aligned slot (so the GPU's 16-B chunks never straddle two packets),
-//   - the matching device arena, descriptor and result buffers,
-//   - its own non-blocking stream and a completion event.
-// A batch is cut into arena-sized pieces; piece k is gathered on the CPU while
-// piece k-1's H2D copy, kernel and D2H copy run on the other slot's stream.
+// i.e. 2 mod 4.  The context's slots, arenas and streams are described in
+// ctx_impl.h; the host frame calls over the same context are frames_host.cpp.
 //
 // One context belongs to one thread at a time (no locks on the hot path):
 // the reference calls checksum() from the core, IPC and timer threads
@@ -23,72 +18,64 @@
 #include <thread>
 #include <vector>
 
-#include "gather_pool.h"
-#include "lvlip_csum.h"
-
-extern "C" int lvlip_csum_batch_dev_ex(const void*, const lvlip_csum_desc*, uint32_t, uint16_t*,
-                                       void*, const lvlip_launch_cfg*);
+#include "ctx_impl.h"
 
 namespace {
 
 constexpr size_t kDefaultArena = 64ull << 20;
 constexpr uint64_t kDirectMax = 4ull << 20;  // measured: DESIGN.md §5
 constexpr uint64_t kPieceMax = 32ull << 20;  // measured: DESIGN.md §5
-constexpr int kSlots = 2;
-
-inline uint64_t align16(uint64_t x) { return (x + 15ull) & ~15ull; }
-
-struct Slot {
-    uint8_t* h_bytes = nullptr;         // pinned
-    lvlip_csum_desc* h_desc = nullptr;  // pinned
-    uint16_t* h_out = nullptr;          // pinned
-    // the same three pinned buffers as device addresses (small pieces are read
-    // and written by the kernel in place, see launch_piece)
-    uint8_t* dh_bytes = nullptr;
-    lvlip_csum_desc* dh_desc = nullptr;
-    uint16_t* dh_out = nullptr;
-    uint8_t* d_bytes = nullptr;
-    lvlip_csum_desc* d_desc = nullptr;
-    uint16_t* d_out = nullptr;
-    hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;
-    // piece bookkeeping
-    uint16_t* user_out = nullptr;  // where results of the in-flight piece go
-    uint32_t count = 0;
-    bool busy = false;
-};
-
-// A registered host region (f3): pinned in place, mapped into the device's
-// address space.
-struct Region {
-    uint8_t* host = nullptr;
-    size_t bytes = 0;
-    uint8_t* dev = nullptr;  // device address of host[0]
-    uint32_t flags = 0;
-};
 
 }  // namespace
 
-struct lvlip_csum_ctx {
-    int device = 0;
-    size_t arena = 0;     // bytes per slot
-    uint32_t max_desc = 0;  // descriptors per slot
-    int threads = 1;        // host threads for the gather into the pinned arena
-    uint64_t direct_max = 0;  // pieces up to this many bytes skip the copies
-    uint64_t piece = 0;       // bytes per piece (<= arena; a larger packet gets its own)
-    Slot slot[kSlots];
-    std::vector<Region> regions;
-    lvlip::GatherPool pool;
-    char err[256] = "";
-};
+namespace lvlip_ctx {
 
-namespace {
-
-int fail(lvlip_csum_ctx* c, hipError_t e, const char* what, int code = LVLIP_EHIP) {
+int fail(lvlip_csum_ctx* c, hipError_t e, const char* what, int code) {
     if (c) snprintf(c->err, sizeof c->err, "%s: %s", what, hipGetErrorString(e));
     fprintf(stderr, "lvlip_csum: %s: %s\n", what, hipGetErrorString(e));
     return code;
 }
+
+int drain(lvlip_csum_ctx* c, Slot& s) {
+    if (!s.busy) return LVLIP_OK;
+    hipError_t e = hipEventSynchronize(s.done);
+    s.busy = false;
+    if (e != hipSuccess) return fail(c, e, "hipEventSynchronize");
+    memcpy(s.user_out, s.h_out, s.out_bytes);
+    return LVLIP_OK;
+}
+
+int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes) {
+    const hipError_t e = hipEventRecord(s.done, s.stream);
+    if (e != hipSuccess) return fail(c, e, "hipEventRecord");
+    s.user_out = user_out;
+    s.out_bytes = out_bytes;
+    s.busy = true;
+    return LVLIP_OK;
+}
+
+int finish_pieces(lvlip_csum_ctx* c, int rc) {
+    for (auto& s : c->slot) {
+        const int r2 = drain(c, s);
+        if (rc == LVLIP_OK) rc = r2;
+    }
+    if (rc != LVLIP_OK)
+        for (auto& s : c->slot) (void)hipStreamSynchronize(s.stream);
+    return rc;
+}
+
+const Region* find_region(const lvlip_csum_ctx* c, const void* p, uint64_t len) {
+    const uint8_t* a = (const uint8_t*)p;
+    for (const Region& r : c->regions)
+        if (a >= r.host && a + len <= r.host + r.bytes) return &r;
+    return nullptr;
+}
+
+}  // namespace lvlip_ctx
+
+namespace {
+
+using namespace lvlip_ctx;
 
 void free_slot(Slot& s) {
     if (s.h_bytes) (void)hipHostFree(s.h_bytes);
@@ -100,16 +87,6 @@ void free_slot(Slot& s) {
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot{};
-}
-
-// Wait for a slot's in-flight piece and hand its results to the caller.
-int drain(lvlip_csum_ctx* c, Slot& s) {
-    if (!s.busy) return LVLIP_OK;
-    hipError_t e = hipEventSynchronize(s.done);
-    s.busy = false;
-    if (e != hipSuccess) return fail(c, e, "hipEventSynchronize");
-    memcpy(s.user_out, s.h_out, (size_t)s.count * sizeof(uint16_t));
-    return LVLIP_OK;
 }
 
 // Copy a piece to the device, checksum it, copy results back.  The bytes come
@@ -130,11 +107,7 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
         const int rc = lvlip_csum_batch_dev_ex(dev_base ? dev_base : s.dh_bytes, s.dh_desc, count,
                                                s.dh_out, s.stream, &cfg);
         if (rc != LVLIP_OK) return rc;
-        if ((e = hipEventRecord(s.done, s.stream)) != hipSuccess) return fail(c, e, "hipEventRecord");
-        s.user_out = user_out;
-        s.count = count;
-        s.busy = true;
-        return LVLIP_OK;
+        return arm_slot(c, s, user_out, (size_t)count * sizeof(uint16_t));
     }
     if (!dev_base) {
         const uint64_t nb = src && src != s.h_bytes ? bytes : align16(bytes);
@@ -151,59 +124,7 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
     if ((e = hipMemcpyAsync(s.h_out, s.d_out, (size_t)count * sizeof(uint16_t),
                             hipMemcpyDeviceToHost, s.stream)) != hipSuccess)
         return fail(c, e, "D2H results");
-    if ((e = hipEventRecord(s.done, s.stream)) != hipSuccess) return fail(c, e, "hipEventRecord");
-    s.user_out = user_out;
-    s.count = count;
-    s.busy = true;
-    return LVLIP_OK;
-}
-
-// End of a batch call: hand over the results still in flight.  After a
-// failure, also wait for whatever a half-enqueued piece left on the slot
-// streams (an H2D copy from the pinned arena, say), so that the next call can
-// reuse the arenas and the caller's buffers are no longer read.
-int finish_pieces(lvlip_csum_ctx* c, int rc) {
-    for (auto& s : c->slot) {
-        const int r2 = drain(c, s);
-        if (rc == LVLIP_OK) rc = r2;
-    }
-    if (rc != LVLIP_OK)
-        for (auto& s : c->slot) (void)hipStreamSynchronize(s.stream);
-    return rc;
-}
-
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
-
-// Run fn(lo, hi) over [0, n) split into up to c->threads contiguous ranges of
-// at least min_per_thread.  The gather into pinned memory is host-memory-
-// bandwidth bound: one core moves ~25-30 GB/s, below PCIe Gen5 x16, so a piece
-// is copied by several of the context's pool threads.
-template <class F>
-void parallel_ranges(lvlip_csum_ctx* c, uint64_t n, uint64_t min_per_thread, F fn) {
-    uint64_t t = c->threads > 1 ? (uint64_t)c->threads : 1u;
-    if (n / min_per_thread < t) t = n / min_per_thread ? n / min_per_thread : 1u;
-    if (t <= 1) {
-        fn(0, n);
-        return;
-    }
-    c->pool.run((int)t, [&](int k) { fn(n * (uint64_t)k / t, n * (uint64_t)(k + 1) / t); });
-}
-
-// The registered region holding [p, p + len), or nullptr.
-const Region* find_region(const lvlip_csum_ctx* c, const void* p, uint64_t len) {
-    const uint8_t* a = (const uint8_t*)p;
-    for (const Region& r : c->regions)
-        if (a >= r.host && a + len <= r.host + r.bytes) return &r;
-    return nullptr;
+    return arm_slot(c, s, user_out, (size_t)count * sizeof(uint16_t));
 }
 
 // Zero-copy: descriptors only (offsets from the region's first byte rounded
@@ -274,6 +195,12 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         const long long v = e ? atoll(e) : (long long)kPieceMax;
         const uint64_t pm = v > 0 ? align16((uint64_t)v) : arena_bytes;
         c->piece = pm < arena_bytes ? pm : arena_bytes;
+    }
+    // LVLIP_FRAME_PATH=hostplan: the host frame calls plan on the CPU (round
+    // 4's path, skb_batch.c) instead of parsing on the device (frames_host.cpp)
+    {
+        const char* e = getenv("LVLIP_FRAME_PATH");
+        c->frame_hostplan = e && strcmp(e, "hostplan") == 0;
     }
     // descriptors per piece: one per 64 B of arena (a piece of smaller packets
     // simply ends at this count; the next piece takes the rest)

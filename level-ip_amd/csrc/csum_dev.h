@@ -1183,8 +1183,9 @@ namespace lvlip {
 
 // f1/f2 on frames in HBM (include/lvlip_skb.h): one k_flat2 launch with a
 // frame source (flat_src.h) per at most kLaunchMax entries, whole frames per
-// launch.  Returns LVLIP_EHIP when a launch fails (the error stays readable by
-// hipGetLastError).
+// launch.  out8 is the verdict / status array, or for FR_TX_REC the u64
+// record array.  Returns LVLIP_EHIP when a launch fails (the error stays
+// readable by hipGetLastError).
 template <int MODE, int U, int GORD, int PFA = 0, int SEC = 0, int STP = 0>
 int launch_frames_flat(const void* base, const lvlip_frame_desc* frames, uint32_t n, uint8_t* out8,
                        hipStream_t s, bool nt_store) {
@@ -1195,6 +1196,10 @@ int launch_frames_flat(const void* base, const lvlip_frame_desc* frames, uint32_
         const uint32_t entries = m * Src::SLOTS;
         const uint32_t grid = (uint32_t)(((uint64_t)entries + FT - 1) / FT);
         Src src{(const uint8_t*)base, (uint8_t*)base, frames + f0, out8 ? out8 + f0 : nullptr};
+        if constexpr (MODE == FR_TX_REC) {
+            src.out8 = nullptr;
+            src.rec = reinterpret_cast<uint64_t*>(out8) + f0;
+        }
         src.nt_store = nt_store;
         hipLaunchKernelGGL((k_flat2<U, true, GORD, Src, 1, false, PFA>), dim3(grid), dim3(FT), 0, s,
                            (const uint8_t*)base, src, entries);

@@ -635,6 +635,24 @@ int lvlip_tx_checksum_dev(void* base, const lvlip_frame_desc* frames, uint32_t n
     return rc;
 }
 
+// The host frame calls' device step (frames_host.cpp; hidden, not part of the
+// ABI): mode 0 TX records (FrameSrc<FR_TX_REC>, the TX fill's shape, u64 per
+// frame into `out`), 1 RX header and 2 RX + L4 (the verdicts, as
+// lvlip_rx_verify_dev).  `base` and `frames` may be device addresses of
+// mapped host memory, and so may `out`.
+int lvlip_frames_host_launch(int mode, const void* base, const lvlip_frame_desc* frames, uint32_t n,
+                             void* out, void* stream) {
+    if (mode == 1) return lvlip_rx_verify_dev(base, frames, n, 0u, (uint8_t*)out, nullptr, stream);
+    if (mode == 2) return lvlip_rx_verify_dev(base, frames, n, LVLIP_RX_VERIFY_L4, (uint8_t*)out, nullptr, stream);
+    if (mode != 0) return LVLIP_EINVAL;
+    if (n == 0) return LVLIP_OK;
+    if (!base || !frames || !out || n > kMaxFrames || ((uintptr_t)base & 15u)) return LVLIP_EINVAL;
+    const int rc = lvlip::launch_frames_flat<lvlip::FR_TX_REC, 8, 2>(base, frames, n, (uint8_t*)out,
+                                                                     (hipStream_t)stream, false);
+    if (rc == LVLIP_EHIP) return hip_fail(hipGetLastError(), "frame call");
+    return rc;
+}
+
 int lvlip_icmp_echo_reply_dev_ex(void* base, const lvlip_frame_desc* frames, uint32_t n, uint32_t flags,
                                  uint8_t* status, void* stream) {
     if (flags & ~LVLIP_ECHO_FULL) return LVLIP_EINVAL;

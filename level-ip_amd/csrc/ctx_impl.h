@@ -1,0 +1,127 @@
+// ctx_impl.h — the host context's internals (include/lvlip_csum.h, Group 3),
+// shared by csum_ctx.cpp (host packet batches) and frames_host.cpp (host frame
+// batches, include/lvlip_skb.h f1/f2).  Not installed; nothing here is
+// exported (the library is built with -fvisibility=hidden).
+//
+// A context owns, per pipeline slot (two slots):
+//   - a pinned host arena the bytes are gathered into (each packet or frame at
+//     a 16-B aligned slot, so the GPU's 16-B chunks never straddle two),
+//   - the matching device arena, descriptor and result buffers,
+//   - its own non-blocking stream and a completion event.
+// A batch is cut into arena-sized pieces; piece k is gathered on the CPU while
+// piece k-1's H2D copy, kernel and D2H copy run on the other slot's stream.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <vector>
+
+#include "gather_pool.h"
+#include "lvlip_csum.h"
+#include "lvlip_skb.h"
+
+namespace lvlip_ctx {
+
+constexpr int kSlots = 2;
+
+inline uint64_t align16(uint64_t x) { return (x + 15ull) & ~15ull; }
+
+struct Slot {
+    uint8_t* h_bytes = nullptr;         // pinned
+    lvlip_csum_desc* h_desc = nullptr;  // pinned (frame calls: lvlip_frame_desc, also 16 B)
+    uint16_t* h_out = nullptr;          // pinned, max_desc u16 (frame calls: records / verdicts)
+    // the same three pinned buffers as device addresses (small pieces are read
+    // and written by the kernel in place, see launch_piece)
+    uint8_t* dh_bytes = nullptr;
+    lvlip_csum_desc* dh_desc = nullptr;
+    uint16_t* dh_out = nullptr;
+    uint8_t* d_bytes = nullptr;
+    lvlip_csum_desc* d_desc = nullptr;
+    uint16_t* d_out = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    // piece bookkeeping: the in-flight piece's results (out_bytes of them in
+    // h_out) go to user_out when the slot drains
+    void* user_out = nullptr;
+    size_t out_bytes = 0;
+    bool busy = false;
+};
+
+// A registered host region (f3): pinned in place, mapped into the device's
+// address space.
+struct Region {
+    uint8_t* host = nullptr;
+    size_t bytes = 0;
+    uint8_t* dev = nullptr;  // device address of host[0]
+    uint32_t flags = 0;
+};
+
+}  // namespace lvlip_ctx
+
+struct lvlip_csum_ctx {
+    int device = 0;
+    size_t arena = 0;         // bytes per slot
+    uint32_t max_desc = 0;    // descriptors per slot (h_out holds 2 B each)
+    int threads = 1;          // host threads for the gather into the pinned arena
+    uint64_t direct_max = 0;  // pieces up to this many bytes skip the copies
+    uint64_t piece = 0;       // bytes per piece (<= arena; a larger packet gets its own)
+    int frame_hostplan = 0;   // LVLIP_FRAME_PATH=hostplan: round 4's host frame path (A/B)
+    lvlip_ctx::Slot slot[lvlip_ctx::kSlots];
+    std::vector<lvlip_ctx::Region> regions;
+    lvlip::GatherPool pool;
+    char err[256] = "";
+};
+
+namespace lvlip_ctx {
+
+// Records a HIP failure in the context (and on stderr); returns `code`.
+int fail(lvlip_csum_ctx* c, hipError_t e, const char* what, int code = LVLIP_EHIP);
+// Waits for a slot's in-flight piece and copies its results to user_out.
+int drain(lvlip_csum_ctx* c, Slot& s);
+// End of a batch call: drains both slots; after a failure also waits for what
+// a half-enqueued piece left on the slot streams.
+int finish_pieces(lvlip_csum_ctx* c, int rc);
+// The registered region holding [p, p + len), or nullptr.
+const Region* find_region(const lvlip_csum_ctx* c, const void* p, uint64_t len);
+// Marks the slot busy with a piece whose results (out_bytes) go to user_out.
+int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes);
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// Runs fn(lo, hi) over [0, n) split into up to c->threads contiguous ranges of
+// at least min_per_thread.  The gather into pinned memory is host-memory-
+// bandwidth bound: one core moves ~25-30 GB/s, below PCIe Gen5 x16, so a piece
+// is copied by several of the context's pool threads.
+template <class F>
+void parallel_ranges(lvlip_csum_ctx* c, uint64_t n, uint64_t min_per_thread, F fn) {
+    uint64_t t = c->threads > 1 ? (uint64_t)c->threads : 1u;
+    if (n / min_per_thread < t) t = n / min_per_thread ? n / min_per_thread : 1u;
+    if (t <= 1) {
+        fn(0, n);
+        return;
+    }
+    c->pool.run((int)t, [&](int k) { fn(n * (uint64_t)k / t, n * (uint64_t)(k + 1) / t); });
+}
+
+}  // namespace lvlip_ctx
+
+extern "C" {
+// csum_kernels.hip
+int lvlip_csum_batch_dev_ex(const void*, const lvlip_csum_desc*, uint32_t, uint16_t*, void*,
+                            const lvlip_launch_cfg*);
+// The host frame calls' device step: mode 0 TX records (u64 per frame), 1 RX
+// header, 2 RX + L4 (u8 verdicts).  Hidden.
+int lvlip_frames_host_launch(int mode, const void* base, const lvlip_frame_desc* frames, uint32_t n,
+                             void* out, void* stream);
+}

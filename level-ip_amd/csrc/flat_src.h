@@ -53,7 +53,14 @@ constexpr uint32_t FR_ETH = 14;
 constexpr uint32_t FR_PENDING = 0x80;   // verdict waits for the header checksum
 constexpr uint32_t FR_HAS_HDR = 0x100;  // plan word: the IPv4 header entry exists
 constexpr uint32_t FR_HAS_L4 = 0x200;   // plan word: the TCP/ICMP entry exists
-enum { FR_TX = 0, FR_RX = 1, FR_RX_L4 = 2 };
+// FR_TX_REC: TX's decisions and sums, but the two fields go to a record per
+// frame instead of into the frame (the host frame calls, frames_host.cpp,
+// apply them to the caller's frames once every frame of the batch is known to
+// be well formed).  Record (u64): bits 0-15 the IPv4 header field, 16-31 the
+// TCP/ICMP field, 32-39 the TCP/ICMP field's offset from the frame's first
+// byte (0 = the frame has no such field), 40-47 status (1 filled, 0 malformed).
+enum { FR_TX = 0, FR_RX = 1, FR_RX_L4 = 2, FR_TX_REC = 3 };
+constexpr bool fr_is_tx(int mode) { return mode == FR_TX || mode == FR_TX_REC; }
 
 __device__ __forceinline__ uint32_t fr_be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
 __device__ __forceinline__ uint32_t fr_le16(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
@@ -253,6 +260,7 @@ struct FrameSrc {
     const lvlip_frame_desc* frames;  // this launch's first frame
     uint8_t* out8;                   // RX: verdict[], TX: status[] (may be null)
     bool nt_store = false;           // TX: nontemporal field stores (the launcher's default)
+    uint64_t* rec = nullptr;         // FR_TX_REC: one record per frame
     static constexpr uint32_t SLOTS = MODE == FR_RX ? 1u : 2u;
     // the frame descriptor of entry i (k_flat2's PFA prefetch: 16 B, like a
     // batch descriptor)
@@ -328,6 +336,7 @@ struct FrameSrc {
         }
         d0 = fr_mk(fd.offset + FR_ETH, ihl * 4u, 0u - x.le16(24));  // src/ip_output.c:42,53
         w |= 1u;
+        if constexpr (MODE == FR_TX_REC) w |= l4 << 24;  // the L4 entry's offset in the frame (<= 74)
         if constexpr (SEC > 0) {
             // which fields' SEC-byte blocks lie wholly inside [frame, frame + len).
             // A field at the last byte of a block straddles two blocks: then
@@ -371,7 +380,7 @@ struct FrameSrc {
         x.load(h, fd.len, reinterpret_cast<uint64_t>(frames + i / SLOTS) & ~15ull);
         lvlip_csum_desc d0 = fr_mk(0, 0, 0), d1 = fr_mk(0, 0, 0);
         w = 0;
-        if (MODE == FR_TX)
+        if (fr_is_tx(MODE))
             parse_tx(fd, h, x, d0, d1, w);
         else
             parse_rx(fd, x, d0, d1, w);
@@ -393,6 +402,20 @@ struct FrameSrc {
     __device__ __forceinline__ void put(uint32_t i, uint16_t c, uint32_t w, bool valid,
                                         uint64_t addr) const {
         const uint32_t f = i / SLOTS;
+        if constexpr (MODE == FR_TX_REC) {
+            // the header lane (slot 2f) writes the frame's record with the L4
+            // lane's result (every lane runs the shuffle)
+            const uint32_t cl4 = (uint32_t)__shfl_xor((int)c, 1, 64) & 0xffffu;
+            if (!valid || (i & 1u)) return;
+            uint64_t r = 0;
+            if (w & 1u) {
+                r = (uint64_t)c | (1ull << 40);
+                if (w & FR_HAS_L4)
+                    r |= ((uint64_t)cl4 << 16) | ((uint64_t)((w >> 24) + ((w >> 16) & 0xffu)) << 32);
+            }
+            rec[f] = r;
+            return;
+        }
         if (MODE == FR_TX) {
             // SEC: the header lane writes a block both fields share, so it
             // takes the L4 lane's result (every lane runs the shuffle)

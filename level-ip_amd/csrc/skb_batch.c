@@ -1,8 +1,11 @@
 /*
  * skb_batch.c — f1/f2 of SURVEY.md §8f: batch-and-dispatch over level-ip frames.
  * See include/lvlip_skb.h for the contract; every decision cites the reference
- * line it mirrors.  Host logic only; the checksums themselves run as one GPU
- * batch through lvlip_csum_batch_host (csum_ctx.cpp).
+ * line it mirrors.  Host logic only: the exported plan/apply steps, f4 on the
+ * host, the skb-queue walkers, and round 4's host-plan frame path (the
+ * checksums as one GPU batch through lvlip_csum_batch_host), which
+ * frames_host.cpp keeps as an A/B under LVLIP_FRAME_PATH=hostplan.  The
+ * product's host frame calls parse on the device (frames_host.cpp).
  */
 #include <pthread.h>
 #include <stddef.h>
@@ -236,8 +239,15 @@ static void rx_apply_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
     lvlip_rx_apply(a->n, a->verdict, a->m[t], a->tag + a->off[t], a->cs + a->off[t]);
 }
 
-int lvlip_rx_verify(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n, uint32_t flags,
-                    uint8_t *verdict)
+/* Round 4's host frame path (hidden; frames_host.cpp runs it under
+ * LVLIP_FRAME_PATH=hostplan): plan every frame on the CPU, one
+ * lvlip_csum_batch_host over the planned pieces, apply. */
+int lvlip_rx_verify_hostplan(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n,
+                             uint32_t flags, uint8_t *verdict);
+int lvlip_tx_checksum_hostplan(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n);
+
+int lvlip_rx_verify_hostplan(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n,
+                             uint32_t flags, uint8_t *verdict)
 {
     /* two checksums per frame at most: 2n must fit one batch (as the _dev call) */
     if (!ctx || (n && (!frames || !verdict)) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
@@ -379,7 +389,7 @@ static void tx_apply_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
     lvlip_tx_apply(a->m[t], a->field + a->off[t], a->cs + a->off[t]);
 }
 
-int lvlip_tx_checksum(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n)
+int lvlip_tx_checksum_hostplan(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n)
 {
     if (!ctx || (n && !frames) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;

@@ -1,0 +1,138 @@
+/*
+ * oracle/ref_txq.c — level-ip's TX path with an optional batch-and-dispatch
+ * step, built from the reference's own compiled objects.  TEST INFRASTRUCTURE
+ * ONLY (north_star: "src/ip_output.c and src/tcp.c ... gain an optional
+ * batch-and-dispatch path over skbuff lists"; VERDICT r04 Next #2).
+ *
+ * oracle/Makefile links _ref/libref_txq.so from the reference objects, with
+ * three of them rewritten by objcopy (our copies; no reference source is
+ * changed or copied):
+ *   tcp.o       tcp_v4_checksum weakened: tcp_transmit_skb's checksum
+ *               (src/tcp_output.c:126) resolves to the deferring one below
+ *   ip_output.o ip_send_check weakened (its call at src/ip_output.c:53 resolves
+ *               below), and its call of dst_neigh_output (src/ip_output.c:55)
+ *               renamed to lvlip_txq_output, the queueing hook below
+ *   icmpv4.o    its checksum() call (src/icmpv4.c:47) renamed to
+ *               lvlip_txq_deferred_checksum
+ * So every frame the stack transmits reaches lvlip_txq_output with its TCP /
+ * ICMP and IPv4 checksum fields zero, exactly as tcp_transmit_skb, icmpv4_reply
+ * and ip_output leave them before summing (src/tcp_output.c:110,
+ * src/icmpv4.c:46, src/ip_output.c:42).
+ *
+ * The hook copies the skb (callers free it when ip_output returns,
+ * src/tcp_output.c:177,264,495, src/icmpv4.c:53; a retransmit queue keeps it)
+ * and links the copy into one sk_buff_head, as skb_queue_tail links skbs
+ * (include/skbuff.h:55-59).  A flush then fills every queued frame's fields in
+ * ONE call, lvlip_tx_checksum_skb_list on the GPU (include/lvlip_skb.h), or
+ * lets the caller fill them (the CPU variant of the test: the oracle's
+ * tx_fill on lvlip_txq_frames' frames), and hands each skb in queue order to
+ * the real dst_neigh_output (src/dst.c:6-30 -> netdev_transmit -> tun_write).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dst.h"
+#include "skbuff.h"
+#include "list.h"
+
+#include "lvlip_skb.h"
+
+#define ETH_LEN 14 /* include/ethernet.h: struct eth_hdr */
+
+static struct sk_buff_head g_txq = {{&g_txq.head, &g_txq.head}, 0};
+static unsigned long g_deferred_sums;
+
+/* src/tcp_output.c:126: the field stays 0 until the flush */
+int tcp_v4_checksum(struct sk_buff *skb, uint32_t saddr, uint32_t daddr)
+{
+    (void)skb, (void)saddr, (void)daddr;
+    g_deferred_sums++;
+    return 0;
+}
+
+/* src/ip_output.c:53: ip_output zeroed the field (:42); it stays 0 */
+void ip_send_check(struct iphdr *ihdr)
+{
+    (void)ihdr;
+    g_deferred_sums++;
+}
+
+/* src/icmpv4.c:47: icmpv4_reply zeroed the field (:46); it stays 0 */
+uint16_t lvlip_txq_deferred_checksum(void *addr, int count, int start_sum)
+{
+    (void)addr, (void)count, (void)start_sum;
+    g_deferred_sums++;
+    return 0;
+}
+
+/* In place of dst_neigh_output (src/ip_output.c:55): queue a copy of the
+ * frame.  Returns what tun_write returns for it (netdev_transmit, the frame's
+ * length with its Ethernet header), or -1 when out of memory. */
+int lvlip_txq_output(struct sk_buff *skb)
+{
+    const unsigned int size = (unsigned int)(skb->end - skb->head);
+    struct sk_buff *c = alloc_skb(size);
+    if (!c) return -1;
+    memcpy(c->head, skb->head, size);
+    c->data = c->head + (skb->data - skb->head);
+    c->len = skb->len;
+    c->dlen = skb->dlen;
+    c->dev = skb->dev;
+    c->rt = skb->rt;
+    c->protocol = skb->protocol;
+    c->seq = skb->seq;
+    c->end_seq = skb->end_seq;
+    skb_queue_tail(&g_txq, c);
+    return (int)(skb->len + ETH_LEN);
+}
+
+int lvlip_txq_len(void) { return (int)g_txq.qlen; }
+
+/* checksum computations the TX path deferred since the last call */
+unsigned long lvlip_txq_deferred(void)
+{
+    const unsigned long d = g_deferred_sums;
+    g_deferred_sums = 0;
+    return d;
+}
+
+/* The queued frames in queue order (the skb's data - 14 .. data + len), for a
+ * caller that fills the fields itself.  Returns the count. */
+int lvlip_txq_frames(lvlip_frame *out, int cap)
+{
+    int k = 0;
+    struct list_head *p;
+    list_for_each(p, &g_txq.head) {
+        struct sk_buff *s = list_entry(p, struct sk_buff, list);
+        if (k < cap) {
+            out[k].head = s->data - ETH_LEN;
+            out[k].len = s->len + ETH_LEN;
+        }
+        k++;
+    }
+    return k;
+}
+
+/* The batch step: every queued frame's checksums in one GPU call.  Returns
+ * the number of frames, or LVLIP_E*. */
+int lvlip_txq_fill_gpu(lvlip_csum_ctx *ctx)
+{
+    return lvlip_tx_checksum_skb_list(ctx, (struct sk_buff_head *)&g_txq);
+}
+
+/* The dispatch step: each queued skb in order to the real dst_neigh_output,
+ * then freed.  Returns the number of frames handed over. */
+int lvlip_txq_send(void)
+{
+    int k = 0;
+    while (g_txq.qlen) {
+        struct sk_buff *s = list_first_entry(&g_txq.head, struct sk_buff, list);
+        list_del(&s->list);
+        g_txq.qlen--;
+        dst_neigh_output(s);
+        free_skb(s);
+        k++;
+    }
+    return k;
+}

@@ -27,7 +27,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 
 run() {  # name, seconds, command...
   local name=$1 secs=$2; shift 2

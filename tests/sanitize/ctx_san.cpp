@@ -3,10 +3,11 @@
 // tests/test_skb_gpu.py::test_host_batches_under_asan).
 //
 // TEST INFRASTRUCTURE ONLY.  tests/sanitize/Makefile compiles the product's
-// own sources (csum_ctx.cpp, skb_batch.c, csum_cpu.c, csum_kernels.hip,
-// skb_dev.hip) with `-Xarch_host -fsanitize=address` into one executable, so
-// the context's pieces, slots, double-buffering, registered regions and the
-// frame calls' host steps run under ASan against real GPU batches.  Every
+// own sources (csum_ctx.cpp, frames_host.cpp, skb_batch.c, csum_cpu.c,
+// csum_kernels.hip) with `-Xarch_host -fsanitize=address` into one executable,
+// so the context's pieces, slots, double-buffering, registered regions and the
+// frame calls' gather, records and apply run under ASan against real GPU
+// batches.  Every
 // packet and frame sits in an allocation that ends at its last byte.  Results
 // are checked against the oracle (oracle/csum_oracle.c).
 #include <hip/hip_runtime.h>
@@ -17,6 +18,7 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <thread>
 #include <vector>
 
@@ -106,37 +108,123 @@ static void flat(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_t see
     free(base);
 }
 
-// f1/f2 frame calls with a real context: exact-size frames, TX then RX.
+// One random well-formed frame (Ethernet + IPv4 ihl 5-7 + TCP or ICMP) at f,
+// flen = frame_len(r) bytes; checksum fields hold junk.
+static uint32_t frame_len(Rng& r, bool& tcp, uint32_t& ihl, uint32_t& l4hdr) {
+    tcp = r() & 1u;
+    ihl = 5u + r() % 3u;
+    l4hdr = tcp ? 20u + 4u * (r() % 6u) : 8u;
+    return 14u + ihl * 4u + l4hdr + r() % 1461u;
+}
+static void fill_frame(Rng& r, uint8_t* f, uint32_t flen, bool tcp, uint32_t ihl, uint32_t l4hdr) {
+    const uint32_t iplen = flen - 14u;
+    for (uint32_t b = 0; b < flen; ++b) f[b] = (uint8_t)r();
+    f[12] = 0x08, f[13] = 0x00;
+    uint8_t* ih = f + 14;
+    ih[0] = (uint8_t)(0x40u | ihl), ih[2] = (uint8_t)(iplen >> 8), ih[3] = (uint8_t)iplen;
+    ih[8] = 64, ih[9] = tcp ? 6 : 1;
+    // 10.0.0.1-120: the reference's u32 pseudo-header sum keeps its carry
+    ih[12] = 10, ih[13] = 0, ih[14] = 0, ih[15] = (uint8_t)(1u + r() % 120u);
+    ih[16] = 10, ih[17] = 0, ih[18] = 0, ih[19] = (uint8_t)(1u + r() % 120u);
+    if (tcp) ih[ihl * 4u + 12u] = (uint8_t)((l4hdr / 4u) << 4);
+}
+
+// TX then RX + L4 over the frames; every header must then sum to zero.
+static void tx_rx_check(lvlip_csum_ctx* ctx, std::vector<lvlip_frame>& fr, const char* what) {
+    const uint32_t n = (uint32_t)fr.size();
+    CHECK(lvlip_tx_checksum(ctx, fr.data(), n) == LVLIP_OK, "%s: tx", what);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* ih = fr[i].head + 14;
+        CHECK(oracle_checksum(ih, (ih[0] & 15) * 4, 0) == 0, "%s: frame %u header", what, i);
+    }
+    std::vector<uint8_t> v(n, 0);
+    for (uint32_t flags = 0; flags <= LVLIP_RX_VERIFY_L4; ++flags) {
+        std::fill(v.begin(), v.end(), 0);
+        CHECK(lvlip_rx_verify(ctx, fr.data(), n, flags, v.data()) == LVLIP_OK, "%s: rx", what);
+        uint32_t ok = 0;
+        for (uint32_t i = 0; i < n; ++i) ok += v[i] == LVLIP_RX_OK;
+        CHECK(ok == n, "%s: rx flags %u: %u of %u ok", what, flags, ok, n);
+    }
+}
+
+// f1/f2 frame calls with a real context: exact-size scattered frames, TX then
+// RX; then one malformed frame in the middle, which must leave every frame
+// untouched.
 static void frame_calls(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed) {
     Rng r{seed};
     std::vector<lvlip_frame> fr(n);
     for (uint32_t i = 0; i < n; ++i) {
-        const bool tcp = r() & 1u;
-        const uint32_t ihl = 5u + r() % 3u, l4hdr = tcp ? 20u + 4u * (r() % 6u) : 8u;
-        const uint32_t iplen = ihl * 4u + l4hdr + r() % 1461u, flen = 14u + iplen;
+        bool tcp;
+        uint32_t ihl, l4hdr;
+        const uint32_t flen = frame_len(r, tcp, ihl, l4hdr);
         uint8_t* f = (uint8_t*)malloc(flen);
-        for (uint32_t b = 0; b < flen; ++b) f[b] = (uint8_t)r();
-        f[12] = 0x08, f[13] = 0x00;
-        uint8_t* ih = f + 14;
-        ih[0] = (uint8_t)(0x40u | ihl), ih[2] = (uint8_t)(iplen >> 8), ih[3] = (uint8_t)iplen;
-        ih[8] = 64, ih[9] = tcp ? 6 : 1;
-        // 10.0.0.1-120: the reference's u32 pseudo-header sum keeps its carry
-        ih[12] = 10, ih[13] = 0, ih[14] = 0, ih[15] = (uint8_t)(1u + r() % 120u);
-        ih[16] = 10, ih[17] = 0, ih[18] = 0, ih[19] = (uint8_t)(1u + r() % 120u);
-        if (tcp) ih[ihl * 4u + 12u] = (uint8_t)((l4hdr / 4u) << 4);
+        fill_frame(r, f, flen, tcp, ihl, l4hdr);
         fr[i] = {f, flen};
     }
-    CHECK(lvlip_tx_checksum(ctx, fr.data(), n) == LVLIP_OK, "tx");
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint8_t* ih = fr[i].head + 14;
-        CHECK(oracle_checksum(ih, (ih[0] & 15) * 4, 0) == 0, "frame %u header", i);
+    tx_rx_check(ctx, fr, "scattered");
+    fr[n / 2].head[14] = 0x65;                   // version 6
+    for (auto& f : fr) f.head[14 + 10] ^= 0x5a;  // stale header fields
+    std::vector<uint8_t> snap;
+    for (auto& f : fr) snap.insert(snap.end(), f.head, f.head + f.len);
+    CHECK(lvlip_tx_checksum(ctx, fr.data(), n) == LVLIP_EINVAL, "malformed refused");
+    size_t o = 0;
+    bool same = true;
+    for (auto& f : fr) {
+        same = same && memcmp(snap.data() + o, f.head, f.len) == 0;
+        o += f.len;
     }
+    CHECK(same, "malformed: frames untouched");
     std::vector<uint8_t> v(n, 0);
-    CHECK(lvlip_rx_verify(ctx, fr.data(), n, LVLIP_RX_VERIFY_L4, v.data()) == LVLIP_OK, "rx");
-    uint32_t ok = 0;
-    for (uint32_t i = 0; i < n; ++i) ok += v[i] == LVLIP_RX_OK;
-    CHECK(ok == n, "rx: %u of %u ok", ok, n);
+    CHECK(lvlip_rx_verify(ctx, fr.data(), n, LVLIP_RX_VERIFY_L4, v.data()) == LVLIP_OK, "rx malformed");
+    CHECK(v[n / 2] == LVLIP_RX_BAD_VERSION, "rx malformed verdict %u", v[n / 2]);
     for (auto& f : fr) free(f.head);
+}
+
+// The same frames packed into one slab (an allocation ending at the last
+// frame's last byte, frames at every alignment, in shuffled order),
+// registered in `reg` mode (DMA: the copy engine reads spans; ZEROCOPY: the
+// kernel reads in place), and as received skbs: BUFLEN-long buffers holding
+// shorter frames (src/netdev.c:89-91), unregistered.
+static void frame_slab(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed, int reg) {
+    Rng r{seed};
+    std::vector<uint32_t> len(n), off(n);
+    std::vector<bool> tcp(n);
+    std::vector<uint32_t> ihl(n), l4h(n);
+    uint64_t pos = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        bool t;
+        len[i] = frame_len(r, t, ihl[i], l4h[i]);
+        tcp[i] = t;
+        pos += r() % 24u;
+        off[i] = (uint32_t)pos;
+        pos += len[i];
+    }
+    uint8_t* slab = (uint8_t*)malloc(pos);
+    for (uint32_t i = 0; i < n; ++i) fill_frame(r, slab + off[i], len[i], tcp[i], ihl[i], l4h[i]);
+    if (reg >= 0) CHECK(lvlip_csum_register(ctx, slab, pos, (uint32_t)reg) == LVLIP_OK, "register frames");
+    std::vector<lvlip_frame> fr(n);
+    for (uint32_t i = 0; i < n; ++i) fr[i] = {slab + off[i], len[i]};
+    for (uint32_t i = n - 1; i > 0; --i) std::swap(fr[i], fr[r() % (i + 1)]);
+    tx_rx_check(ctx, fr, reg < 0 ? "slab" : reg == (int)LVLIP_REG_DMA ? "slab dma" : "slab zerocopy");
+    if (reg >= 0) CHECK(lvlip_csum_unregister(ctx, slab) == LVLIP_OK, "unregister frames");
+    // as skbs from netdev_rx_loop: the frame at the start of a 1600-B buffer,
+    // the buffer's end as the frame's end
+    if (reg < 0) {
+        const uint32_t buflen = 1600, m = n < 2000 ? n : 2000;
+        uint8_t* skbs = (uint8_t*)calloc((size_t)m, buflen);
+        std::vector<lvlip_frame> sk(m);
+        for (uint32_t i = 0; i < m; ++i) {
+            const uint32_t l = len[i] < buflen ? len[i] : buflen;
+            memcpy(skbs + (size_t)i * buflen, slab + off[i], l);
+            sk[i] = {skbs + (size_t)i * buflen, buflen};
+        }
+        std::vector<uint8_t> v(m, 0);
+        CHECK(lvlip_rx_verify(ctx, sk.data(), m, LVLIP_RX_VERIFY_L4, v.data()) == LVLIP_OK, "rx skbs");
+        for (uint32_t i = 0; i < m; ++i)
+            CHECK(v[i] == (len[i] <= buflen ? LVLIP_RX_OK : LVLIP_RX_SHORT), "rx skb %u: %u", i, v[i]);
+        free(skbs);
+    }
+    free(slab);
 }
 
 int main() {
@@ -153,6 +241,9 @@ int main() {
     flat(ctx, 20000, 1600, 4, (int)LVLIP_REG_DMA);
     flat(ctx, 5000, 1600, 5, (int)LVLIP_REG_ZEROCOPY);
     frame_calls(ctx, 20000, 6);
+    frame_slab(ctx, 20000, 7, -1);
+    frame_slab(ctx, 20000, 8, (int)LVLIP_REG_DMA);
+    frame_slab(ctx, 5000, 9, (int)LVLIP_REG_ZEROCOPY);
 
     // a packet larger than the arena is refused; nothing is read
     std::vector<uint8_t> big((2u << 20) + 5u, 0xab);

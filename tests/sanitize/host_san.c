@@ -13,8 +13,11 @@
  *   2. eight threads calling checksum / tcp_udp_checksum at once (the
  *      reference calls checksum() from its core, IPC and timer threads);
  *   3. 40 000 frames, each in an allocation of exactly its length, through
- *      lvlip_tx_checksum and lvlip_rx_verify (several host threads), plus
- *      malformed frames that must be refused without reading past their ends.
+ *      the host-plan frame path (skb_batch.c's lvlip_tx_checksum_hostplan and
+ *      lvlip_rx_verify_hostplan, several host threads; the product's
+ *      lvlip_tx_checksum / lvlip_rx_verify run it under
+ *      LVLIP_FRAME_PATH=hostplan), plus malformed frames that must be refused
+ *      without reading past their ends.
  *
  * The GPU batch between the host steps (lvlip_csum_batch_host, csum_ctx.cpp)
  * is replaced below by the oracle: the host code around it is what is under
@@ -33,6 +36,11 @@ uint32_t oracle_sum_every_16bits(const void *addr, int count);
 uint16_t oracle_checksum(const void *addr, int count, int start_sum);
 int oracle_tcp_udp_checksum(uint32_t saddr, uint32_t daddr, uint8_t proto, const uint8_t *data,
                             uint16_t len);
+
+/* skb_batch.c (hidden in the library) */
+int lvlip_rx_verify_hostplan(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n,
+                             uint32_t flags, uint8_t *verdict);
+int lvlip_tx_checksum_hostplan(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n);
 
 static int g_fail;
 #define CHECK(c, ...)                                            \
@@ -53,6 +61,18 @@ int lvlip_csum_batch_host(lvlip_csum_ctx *ctx, const lvlip_csum_iov *p, uint32_t
     for (uint32_t i = 0; i < n; i++)
         out[i] = oracle_checksum(p[i].ptr, p[i].len, (int)p[i].start_sum);
     return LVLIP_OK;
+}
+
+/* stand-ins for the product's frame calls (frames_host.cpp, HIP host code),
+ * which skb_batch.c's skb-queue walkers call: the host-plan path here */
+int lvlip_rx_verify(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n, uint32_t flags,
+                    uint8_t *verdict)
+{
+    return lvlip_rx_verify_hostplan(ctx, frames, n, flags, verdict);
+}
+int lvlip_tx_checksum(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n)
+{
+    return lvlip_tx_checksum_hostplan(ctx, frames, n);
 }
 
 static uint64_t g_rng = 0x1E7E1C5ull;
@@ -167,7 +187,7 @@ static void frames(void)
     for (uint32_t i = 0; i < n; i++) fr[i] = make_frame((rnd() & 1u) != 0);
     lvlip_csum_ctx *ctx = (lvlip_csum_ctx *)(void *)&g_fail; /* opaque, unused by the stand-in */
 
-    CHECK(lvlip_tx_checksum(ctx, fr, n) == LVLIP_OK, "tx");
+    CHECK(lvlip_tx_checksum_hostplan(ctx, fr, n) == LVLIP_OK, "tx");
     for (uint32_t i = 0; i < n; i++) {
         uint8_t *ih = fr[i].head + 14;
         const uint32_t ihl = ih[0] & 15u, iplen = ((uint32_t)ih[2] << 8) | ih[3];
@@ -191,7 +211,7 @@ static void frames(void)
     uint8_t *v = (uint8_t *)malloc(n);
     for (uint32_t flags = 0; flags <= LVLIP_RX_VERIFY_L4; flags++) {
         memset(v, 0, n);
-        CHECK(lvlip_rx_verify(ctx, fr, n, flags, v) == LVLIP_OK, "rx");
+        CHECK(lvlip_rx_verify_hostplan(ctx, fr, n, flags, v) == LVLIP_OK, "rx");
         uint32_t ok = 0;
         for (uint32_t i = 0; i < n; i++) ok += v[i] == LVLIP_RX_OK;
         CHECK(ok == n, "rx flags %u: %u of %u ok", flags, ok, n);
@@ -223,11 +243,11 @@ static void frames(void)
         if (k != 6 && k != 7) { /* 6 and 7 are well-formed IPv4 as far as TX cares */
             uint8_t *snap = (uint8_t *)malloc(bad.len);
             memcpy(snap, bad.head, bad.len);
-            CHECK(lvlip_tx_checksum(ctx, fr, n) == LVLIP_EINVAL, "tx kind %u refused", k);
+            CHECK(lvlip_tx_checksum_hostplan(ctx, fr, n) == LVLIP_EINVAL, "tx kind %u refused", k);
             CHECK(memcmp(snap, bad.head, bad.len) == 0, "tx kind %u untouched", k);
             free(snap);
         }
-        CHECK(lvlip_rx_verify(ctx, fr, n, LVLIP_RX_VERIFY_L4, v) == LVLIP_OK, "rx kind %u", k);
+        CHECK(lvlip_rx_verify_hostplan(ctx, fr, n, LVLIP_RX_VERIFY_L4, v) == LVLIP_OK, "rx kind %u", k);
         if (want_rx != 0xff)
             CHECK(v[at] == want_rx, "rx kind %u: verdict %u want %u", k, v[at], want_rx);
         else
@@ -236,9 +256,9 @@ static void frames(void)
         free(bad.head);
         fr[at] = keep;
     }
-    CHECK(lvlip_rx_verify(ctx, fr, 0, 0, v) == LVLIP_OK && lvlip_tx_checksum(ctx, fr, 0) == LVLIP_OK,
+    CHECK(lvlip_rx_verify_hostplan(ctx, fr, 0, 0, v) == LVLIP_OK && lvlip_tx_checksum_hostplan(ctx, fr, 0) == LVLIP_OK,
           "n = 0");
-    CHECK(lvlip_rx_verify(NULL, fr, n, 0, v) == LVLIP_EINVAL, "NULL ctx");
+    CHECK(lvlip_rx_verify_hostplan(NULL, fr, n, 0, v) == LVLIP_EINVAL, "NULL ctx");
     for (uint32_t i = 0; i < n; i++) free(fr[i].head);
     free(fr);
     free(v);

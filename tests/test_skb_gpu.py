@@ -127,6 +127,139 @@ def test_empty(ctx):
     ctx.tx_checksum([])
 
 
+# ------------------------------------- host frames: every source (round 5) --
+#
+# The host frame calls parse on the device (frames_host.cpp): scattered frames
+# are gathered whole into the pinned arena, frames in a registered region are
+# DMA'd as spans (LVLIP_REG_DMA) or read in place (LVLIP_REG_ZEROCOPY).  The
+# same frames through every source must give the oracle's verdicts and fill.
+
+SOURCES = ("scattered", "slab", "dma", "zerocopy")
+
+
+def _frames_in(source, frames, seed):
+    """(views, buf): the frames as separate bytearrays ("scattered"), or as
+    numpy views into one slab (frames at every offset mod 16, in shuffled
+    order), unregistered or to be registered."""
+    if source == "scattered":
+        return [bytearray(f) for f in frames], None
+    buf, fd = lvlip.pack_frames(frames, align_mod=16, seed=seed)
+    views = [buf[int(d["offset"]):int(d["offset"]) + int(d["len"])] for d in fd]
+    return views, buf
+
+
+def _registered(ctx, source, buf):
+    if source in ("dma", "zerocopy"):
+        ctx.register(buf, lvlip.REG_DMA if source == "dma" else lvlip.REG_ZEROCOPY)
+
+
+def _unregister(ctx, source, buf):
+    if source in ("dma", "zerocopy"):
+        ctx.unregister(buf)
+
+
+@pytest.mark.parametrize("source", SOURCES)
+def test_host_frames_every_source_matches_oracle(ctx, source):
+    """20 000 frames (options, odd lengths, 300 jumbo) filled by the TX call,
+    then 2 000 bit flips and 200 truncations plus every ip_rcv drop reason:
+    TX fill == the oracle's fill and the RX verdicts (header, header + L4) ==
+    the oracle's, through each source, the order shuffled so the DMA spans
+    run out of address order."""
+    fr = workloads.frames(20000, seed=81, max_l4=1460) + workloads.frames(300, seed=82, max_l4=8900)
+    want = [bytearray(f) for f in fr]
+    for f in want:
+        skb_oracle.tx_fill(f)
+    views, buf = _frames_in(source, fr, seed=83)
+    rng = np.random.default_rng(84)
+    perm = rng.permutation(len(views))
+    _registered(ctx, source, buf)
+    try:
+        ctx.tx_checksum([views[int(i)] for i in perm])
+        got = [bytes(v) for v in views]
+        bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != bytes(w)]
+        assert not bad, bad[:10]
+        for i in rng.choice(len(views), 2000, replace=False):
+            v = views[int(i)]
+            v[14 + int(rng.integers(0, len(v) - 14))] ^= 0x10
+        rx = [views[int(i)] for i in perm]
+        for i in rng.choice(len(rx), 200, replace=False):
+            rx[int(i)] = rx[int(i)][: int(rng.integers(0, 80))]
+        cases = _rx_cases(85)
+        for flags in (0, lvlip.RX_VERIFY_L4):
+            v = ctx.rx_verify(rx, flags)
+            w = np.array([skb_oracle.rx_verdict(bytes(f), flags) for f in rx], dtype=np.uint8)
+            assert np.array_equal(v, w), (flags, np.nonzero(v != w)[0][:5])
+            # the drop reasons, scattered, in the same call as slab frames
+            v = ctx.rx_verify(rx[:3000] + cases, flags)
+            w = [skb_oracle.rx_verdict(bytes(f), flags) for f in rx[:3000] + cases]
+            assert v.tolist() == w, flags
+    finally:
+        _unregister(ctx, source, buf)
+
+
+@pytest.mark.parametrize("source", SOURCES)
+def test_host_tx_malformed_untouched_every_source(ctx, source):
+    """One malformed frame (version 6) among 5 000: LVLIP_EINVAL and every
+    frame byte unchanged, whichever source the frames come from (the device
+    fills records, the host stores nothing until all are well formed)."""
+    fr = workloads.frames(5000, seed=86, max_l4=1460)
+    views, buf = _frames_in(source, fr, seed=87)
+    views[2500][14] = 0x65
+    before = [bytes(v) for v in views]
+    _registered(ctx, source, buf)
+    try:
+        with pytest.raises(lvlip.LvlipError) as ei:
+            ctx.tx_checksum(views)
+        assert ei.value.rc == lvlip.EINVAL
+        assert [bytes(v) for v in views] == before
+    finally:
+        _unregister(ctx, source, buf)
+
+
+def test_rx_verify_skb_buffers_longer_than_frames(ctx):
+    """RX skbs as netdev_rx_loop fills them: every frame at the start of a
+    BUFLEN (1600 B) buffer whose end is the frame's end (src/netdev.c:89-91),
+    the bytes past the IP total length garbage.  The gather moves only
+    max(74, 14 + total length) bytes of each; the verdicts == the oracle's on
+    the whole buffers, with total lengths below, at and above the buffer."""
+    rng = np.random.default_rng(88)
+    fr = workloads.frames(6000, seed=89, max_l4=1400)
+    for f in fr:
+        skb_oracle.tx_fill(f)
+    for i in rng.choice(len(fr), 600, replace=False):
+        f = fr[int(i)]
+        f[14 + int(rng.integers(0, len(f) - 14))] ^= 0x04
+    for i in rng.choice(len(fr), 100, replace=False):  # total length past the buffer
+        fr[int(i)][16:18] = int(rng.integers(1600 - 14 + 1, 65536)).to_bytes(2, "big")
+    bufs = []
+    for f in fr:
+        b = bytearray(rng.integers(0, 256, 1600, dtype=np.uint8).tobytes())
+        b[:len(f)] = f
+        bufs.append(b)
+    for flags in (0, lvlip.RX_VERIFY_L4):
+        got = ctx.rx_verify(bufs, flags)
+        want = np.array([skb_oracle.rx_verdict(bytes(b), flags) for b in bufs], dtype=np.uint8)
+        assert np.array_equal(got, want), (flags, np.nonzero(got != want)[0][:5])
+    assert (got == lvlip.RX_OK).sum() > 4000
+
+
+def test_host_frames_hostplan_ab_agrees(monkeypatch):
+    """LVLIP_FRAME_PATH=hostplan (round 4's host path, kept for A/B) and the
+    product's device-parse path give the same fill and verdicts."""
+    fr = workloads.frames(8000, seed=92, max_l4=1460)
+    a, b = [bytearray(f) for f in fr], [bytearray(f) for f in fr]
+    monkeypatch.setenv("LVLIP_FRAME_PATH", "hostplan")
+    with lvlip.Context(0, arena_bytes=4 << 20) as hp:
+        hp.tx_checksum(a)
+        va = [hp.rx_verify(a, fl) for fl in (0, lvlip.RX_VERIFY_L4)]
+    monkeypatch.delenv("LVLIP_FRAME_PATH")
+    with lvlip.Context(0, arena_bytes=4 << 20) as dp:
+        dp.tx_checksum(b)
+        vb = [dp.rx_verify(b, fl) for fl in (0, lvlip.RX_VERIFY_L4)]
+    assert [bytes(x) for x in a] == [bytes(x) for x in b]
+    assert all(np.array_equal(x, y) for x, y in zip(va, vb))
+
+
 # ------------------------------------------------- device-resident frames --
 
 def _dev(buf):
