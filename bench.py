@@ -651,11 +651,11 @@ def sweep(lvlip, torch, base, descs, out, b, stream):
     return res
 
 
-def frames_dev(lvlip, torch, dev):
-    """Device-resident frame batches (diagnostic, include/lvlip_skb.h): the mixed
-    config's 2M frames made valid IPv4/TCP/ICMP frames in HBM, then TX fill,
-    RX verify (header) and RX verify with L4, each timed with HIP events on
-    the launch stream.  GB/s counts the checksummed bytes of each call."""
+def mixed_frames_hbm(lvlip, torch, dev):
+    """The mixed config's 2M frames made valid IPv4/TCP/ICMP frames in HBM
+    (Ethernet type, version/ihl, total length, TTL, protocol written into each
+    frame's header): (uint8 CUDA tensor, FRAME_DESC_DTYPE descriptors, the
+    payload descriptors)."""
     import workloads
 
     b = workloads.make("mixed")
@@ -675,6 +675,16 @@ def frames_dev(lvlip, torch, dev):
     fd = np.zeros(n, dtype=lvlip.FRAME_DESC_DTYPE)
     fd["offset"] = hdr["offset"] - 14
     fd["len"] = 34 + pay["len"]
+    return base, fd, pay
+
+
+def frames_dev(lvlip, torch, dev):
+    """Device-resident frame batches (diagnostic, include/lvlip_skb.h): the mixed
+    config's 2M frames made valid IPv4/TCP/ICMP frames in HBM, then TX fill,
+    RX verify (header) and RX verify with L4, each timed with HIP events on
+    the launch stream.  GB/s counts the checksummed bytes of each call."""
+    base, fd, pay = mixed_frames_hbm(lvlip, torch, dev)
+    n = fd.size
     fdt = torch.from_numpy(fd.view(np.uint8).copy()).to(dev)
     stream = torch.cuda.current_stream(dev)
     l4_bytes = int(pay["len"].sum())
@@ -720,6 +730,8 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
       zerocopy   the slab registered LVLIP_REG_ZEROCOPY (kernel reads in place)
       hostplan   the slab through round 4's path (LVLIP_FRAME_PATH=hostplan:
                  the CPU plans every frame, two gathered pieces per frame)
+      scattered_t16  scattered with 16 gather threads (LVLIP_GATHER_THREADS;
+                 the default is 8)
     GB/s counts the checksummed bytes (20 B header + L4 per frame) as the
     device lines do; frame_GBps counts the frames' bytes (what crosses PCIe)."""
     import ctypes
@@ -780,12 +792,15 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
                 run(ctx, keep_slab[1], tag)
             finally:
                 ctx.unregister(host)
-    os.environ["LVLIP_FRAME_PATH"] = "hostplan"
-    try:
-        with lvlip.Context(d) as ctx:
-            run(ctx, keep_slab[1], "hostplan")
-    finally:
-        del os.environ["LVLIP_FRAME_PATH"]
+    for env, tag, arr in (("LVLIP_FRAME_PATH=hostplan", "hostplan", keep_slab[1]),
+                          ("LVLIP_GATHER_THREADS=16", "scattered_t16", keep_scat[1])):
+        k, v = env.split("=")
+        os.environ[k] = v
+        try:
+            with lvlip.Context(d) as ctx:
+                run(ctx, arr, tag)
+        finally:
+            del os.environ[k]
     # the frames the TX calls filled are what the HBM frames hold after
     # tx_fill (same bytes, same fill): spot-check the slab against the scatter
     for i in range(0, n, max(1, n // 997)):

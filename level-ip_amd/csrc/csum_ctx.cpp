@@ -178,7 +178,7 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
     {
         const char* e = getenv("LVLIP_GATHER_THREADS");
         const unsigned hw = std::thread::hardware_concurrency();
-        int t = e ? atoi(e) : (int)(hw ? (hw < 8 ? hw : 8) : 1);
+        int t = e ? atoi(e) : (int)(hw ? (hw < 16 ? hw : 16) : 1);
         c->threads = t < 1 ? 1 : (t > 64 ? 64 : t);
     }
     // LVLIP_DIRECT_MAX: pieces of at most this many bytes skip the H2D/D2H
@@ -195,6 +195,14 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         const long long v = e ? atoll(e) : (long long)kPieceMax;
         const uint64_t pm = v > 0 ? align16((uint64_t)v) : arena_bytes;
         c->piece = pm < arena_bytes ? pm : arena_bytes;
+    }
+    // LVLIP_FIRST_PIECE: the host frame calls' first piece, in bytes; later
+    // pieces double up to the piece size (0 or unset: 4 MiB; a value >= the
+    // piece size turns the ramp off)
+    {
+        const char* e = getenv("LVLIP_FIRST_PIECE");
+        const long long v = e ? atoll(e) : 0;
+        c->first_piece = v > 0 ? align16((uint64_t)v) : (4ull << 20);
     }
     // LVLIP_FRAME_PATH=hostplan: the host frame calls plan on the CPU (round
     // 4's path, skb_batch.c) instead of parsing on the device (frames_host.cpp)
@@ -240,6 +248,8 @@ int lvlip_csum_ctx_destroy(lvlip_csum_ctx* c) {
         free_slot(s);
     }
     for (const Region& r : c->regions) (void)hipHostUnregister(r.host);
+    free(c->frame_scratch);
+    free(c->frame_scratch2);
     delete c;
     return LVLIP_OK;
 }

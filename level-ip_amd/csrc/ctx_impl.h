@@ -67,6 +67,13 @@ struct lvlip_csum_ctx {
     int threads = 1;          // host threads for the gather into the pinned arena
     uint64_t direct_max = 0;  // pieces up to this many bytes skip the copies
     uint64_t piece = 0;       // bytes per piece (<= arena; a larger packet gets its own)
+    uint64_t first_piece = 0; // frame calls: the first piece's bytes (doubling up to `piece`)
+    // frame calls' per-call host arrays (TX records and undo values, RX + L4
+    // lengths), kept across calls: fresh pages would fault on every call
+    void* frame_scratch = nullptr;
+    size_t frame_scratch_bytes = 0;
+    void* frame_scratch2 = nullptr;
+    size_t frame_scratch2_bytes = 0;
     int frame_hostplan = 0;   // LVLIP_FRAME_PATH=hostplan: round 4's host frame path (A/B)
     lvlip_ctx::Slot slot[lvlip_ctx::kSlots];
     std::vector<lvlip_ctx::Region> regions;

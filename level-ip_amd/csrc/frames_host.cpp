@@ -31,8 +31,14 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <emmintrin.h>
+
+#include <algorithm>
+#include <chrono>
 
 #include "ctx_impl.h"
 
@@ -56,6 +62,8 @@ constexpr uint32_t kHdrWin = kEth + 60;
 inline uint32_t out_bytes(int mode) { return mode == M_TX ? 8u : 1u; }
 
 inline uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+// frames ahead whose first lines the gather and the apply prefetch
+constexpr uint64_t kPrefetch = 8;
 
 // The bytes of a frame the device step reads, so the gather moves no more.
 // Every decision the kernels take compares the frame length with 14 + 20,
@@ -77,11 +85,116 @@ inline uint32_t need_len(int mode, const lvlip_frame& f) {
     return f.len;
 }
 
+// The context's scratch array of at least `bytes` (kept for later calls).
+void* scratch(lvlip_csum_ctx* c, size_t bytes) {
+    if (c->frame_scratch_bytes < bytes) {
+        free(c->frame_scratch);
+        c->frame_scratch = malloc(bytes);
+        c->frame_scratch_bytes = c->frame_scratch ? bytes : 0;
+    }
+    return c->frame_scratch;
+}
+
+// A second scratch array (the gather's prefix sums and RX + L4's lengths),
+// kept like the first.
+void* scratch2(lvlip_csum_ctx* c, size_t bytes) {
+    if (c->frame_scratch2_bytes < bytes) {
+        free(c->frame_scratch2);
+        c->frame_scratch2 = malloc(bytes);
+        c->frame_scratch2_bytes = c->frame_scratch2 ? bytes : 0;
+    }
+    return c->frame_scratch2;
+}
+
+// One frame into its 16-B aligned arena slot with nontemporal 16-B stores.
+// The copy engine reads the arena next: stores that bypass the CPU caches
+// leave no dirty lines for its reads to snoop, and need no read-for-ownership
+// of the slot's lines (measured).  The last partial chunk goes
+// through a zeroed 16-B temporary (nothing past the frame's end is read; the
+// slot's padding bytes become zero).  The caller fences (_mm_sfence) before
+// the copy engine is started.
+inline void copy_frame_nt(uint8_t* dst, const uint8_t* src, uint32_t len) {
+    uint32_t k = 0;
+    for (; k + 64 <= len; k += 64) {
+        const __m128i a = _mm_loadu_si128((const __m128i*)(src + k));
+        const __m128i b = _mm_loadu_si128((const __m128i*)(src + k + 16));
+        const __m128i c = _mm_loadu_si128((const __m128i*)(src + k + 32));
+        const __m128i d = _mm_loadu_si128((const __m128i*)(src + k + 48));
+        _mm_stream_si128((__m128i*)(dst + k), a);
+        _mm_stream_si128((__m128i*)(dst + k + 16), b);
+        _mm_stream_si128((__m128i*)(dst + k + 32), c);
+        _mm_stream_si128((__m128i*)(dst + k + 48), d);
+    }
+    for (; k + 16 <= len; k += 16) _mm_stream_si128((__m128i*)(dst + k), _mm_loadu_si128((const __m128i*)(src + k)));
+    if (k < len) {
+        alignas(16) uint8_t t[16] = {0};
+        memcpy(t, src + k, len - k);
+        _mm_stream_si128((__m128i*)(dst + k), _mm_load_si128((const __m128i*)t));
+    }
+}
+
 // Frames per piece: the slot's descriptor array and its result buffer.
 inline uint32_t frames_per_piece(const lvlip_csum_ctx* c, int mode) {
     const uint64_t by_out = (uint64_t)c->max_desc * sizeof(uint16_t) / out_bytes(mode);
     return by_out < c->max_desc ? (uint32_t)by_out : c->max_desc;
 }
+
+// Bytes of piece number `idx` of a call: the pipeline starts with small
+// pieces (the GPU waits for the first gather or copy, and the first piece's
+// results gate the host's first apply), doubling from the context's
+// first_piece (LVLIP_FIRST_PIECE, 4 MiB) up to its piece size
+// (LVLIP_PIECE_MAX, 32 MiB).
+inline uint64_t piece_bytes(const lvlip_csum_ctx* c, uint32_t idx) {
+    const uint64_t r = idx < 16 ? c->first_piece << idx : c->piece;
+    return r < c->piece ? r : c->piece;
+}
+
+// LVLIP_FRAME_TRACE=1: one line per call on stderr with the host's time in
+// each step (diagnostics for the pipeline's balance; off by default).
+struct Trace {
+    bool on = false;
+    std::chrono::steady_clock::time_point t0;
+    double pass1 = 0, gather = 0, wait = 0, apply = 0;
+    uint32_t pieces = 0;
+    static double ms(std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+    }
+};
+thread_local Trace g_trace;
+
+// Called with each piece's frame range once its results are in the caller's
+// array (TX: the host applies that piece's records while later pieces run).
+struct PieceDone {
+    virtual void done(uint32_t first, uint32_t k) = 0;
+};
+
+// drain() plus the piece callback; the slot remembers its piece's range.
+struct FrameSlots {
+    lvlip_csum_ctx* c;
+    PieceDone* cb;
+    uint32_t first[kSlots] = {0, 0}, count[kSlots] = {0, 0};
+    int drain_slot(int k) {
+        Slot& s = c->slot[k];
+        const bool was = s.busy;
+        auto t = std::chrono::steady_clock::now();
+        const int rc = drain(c, s);
+        if (g_trace.on) g_trace.wait += Trace::ms(t);
+        t = std::chrono::steady_clock::now();
+        if (rc == LVLIP_OK && was && cb) cb->done(first[k], count[k]);
+        if (g_trace.on && was) g_trace.apply += Trace::ms(t), g_trace.pieces++;
+        return rc;
+    }
+    // finish_pieces with the callback: the older piece first
+    int finish(int rc, int next) {
+        for (int j = 0; j < kSlots; ++j) {
+            const int r2 = drain_slot((next + j) % kSlots);
+            if (rc == LVLIP_OK) rc = r2;
+        }
+        if (rc != LVLIP_OK)
+            for (auto& s : c->slot) (void)hipStreamSynchronize(s.stream);
+        return rc;
+    }
+};
 
 // One piece of k frames (descriptors in the slot's pinned h_desc) through the
 // device step, as csum_ctx.cpp's launch_piece: the frames come from the
@@ -117,108 +230,138 @@ int launch_frame_piece(lvlip_csum_ctx* c, Slot& s, int mode, uint64_t bytes, uin
 }
 
 // Scattered frames: each frame's need_len bytes (len[i] when given) copied
-// whole into the next 16-B aligned slot of the pinned arena.
+// whole into its 16-B aligned slot of the pinned arena.  pre[i] is frame i's
+// slot offset in the batch's virtual arena stream (pre[n] the total), so a
+// piece is the run of frames whose slots fit the piece, found by binary
+// search, and the pool threads write its descriptors as they copy.
 int frames_gather(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out,
-                  const uint32_t* len) {
+                  const uint32_t* len, const uint64_t* pre, PieceDone* cb) {
     const uint32_t fmax = frames_per_piece(c, mode), ob = out_bytes(mode);
+    FrameSlots fs{c, cb};
     int cur = 0;
-    uint32_t i = 0;
+    uint32_t i = 0, idx = 0;
     int rc = LVLIP_OK;
     while (i < n && rc == LVLIP_OK) {
         Slot& s = c->slot[cur];
-        if ((rc = drain(c, s)) != LVLIP_OK) break;
+        if ((rc = fs.drain_slot(cur)) != LVLIP_OK) break;
         lvlip_frame_desc* hd = (lvlip_frame_desc*)s.h_desc;
-        uint64_t off = 0;
-        uint32_t k = 0;
         const uint32_t first = i;
-        while (i < n && k < fmax) {
-            const uint32_t l = len ? len[i] : need_len(mode, fr[i]);
-            if (off + l > (k ? c->piece : c->arena)) break;  // k = 0: fits (checked by the caller)
-            hd[k].offset = off;
-            hd[k].len = l;
-            hd[k].reserved = 0;
-            off = align16(off + l);
-            ++k;
-            ++i;
-        }
+        const uint64_t pb = piece_bytes(c, idx++);
+        // the last frame whose slot ends within pb of the piece's start
+        const uint32_t cap = n - first < fmax ? n : first + fmax;
+        uint32_t e = (uint32_t)(std::upper_bound(pre + first + 1, pre + cap + 1, pre[first] + pb) - pre) - 1;
+        if (e == first) e = first + 1;  // one frame larger than a piece: alone (it fits the arena)
+        const uint32_t k = e - first;
+        const uint64_t off = pre[e] - pre[first];
+        i = e;
         {
+            const auto t = std::chrono::steady_clock::now();
             uint8_t* dst = s.h_bytes;
             const lvlip_frame* src = fr + first;
+            const uint64_t* pf = pre + first;
+            const uint32_t* lf = len ? len + first : nullptr;
             parallel_ranges(c, k, 256, [=](uint64_t lo, uint64_t hi) {
-                for (uint64_t q = lo; q < hi; ++q)
-                    if (hd[q].len) memcpy(dst + hd[q].offset, src[q].head, hd[q].len);
+                for (uint64_t q = lo; q < hi; ++q) {
+                    // scattered frames: the whole frame kPrefetch frames ahead
+                    // (scattered 1616-B slots: +25-40 % over its first two lines)
+                    const uint64_t pq = q + kPrefetch;
+                    if (pq < hi && src[pq].head)
+                        for (uint32_t l = 0; l < src[pq].len; l += 64) __builtin_prefetch(src[pq].head + l);
+                    const uint32_t l = lf ? lf[q] : need_len(mode, src[q]);
+                    hd[q].offset = pf[q] - pf[0];
+                    hd[q].len = l;
+                    hd[q].reserved = 0;
+                    if (l) copy_frame_nt(dst + hd[q].offset, src[q].head, l);
+                }
+                _mm_sfence();  // the nontemporal stores land before the copy engine reads
             });
+            if (g_trace.on) g_trace.gather += Trace::ms(t);
         }
+        fs.first[cur] = first;
+        fs.count[cur] = k;
         rc = launch_frame_piece(c, s, mode, off ? off : 16, k, out + (size_t)first * ob);
         cur ^= 1;
     }
-    return finish_pieces(c, rc);
+    return fs.finish(rc, cur);
+}
+
+// Frame descriptors {head - base, len} of k frames, on the pool threads.
+void write_descs(lvlip_csum_ctx* c, lvlip_frame_desc* hd, const lvlip_frame* f, uint32_t k, uintptr_t base) {
+    parallel_ranges(c, k, 8192, [=](uint64_t lo, uint64_t hi) {
+        for (uint64_t q = lo; q < hi; ++q) {
+            hd[q].offset = (uint64_t)((uintptr_t)f[q].head - base);
+            hd[q].len = f[q].len;
+            hd[q].reserved = 0;
+        }
+    });
 }
 
 // Frames inside one LVLIP_REG_ZEROCOPY region: descriptors only, offsets from
 // the region's first byte rounded down to 16; the kernel reads in place.
 int frames_zerocopy(lvlip_csum_ctx* c, const Region& r, const lvlip_frame* fr, uint32_t n, int mode,
-                    uint8_t* out) {
+                    uint8_t* out, PieceDone* cb) {
     const uint8_t* h0 = (const uint8_t*)((uintptr_t)r.host & ~(uintptr_t)15);
     const uint8_t* d0 = r.dev - (r.host - h0);
     const uint32_t fmax = frames_per_piece(c, mode), ob = out_bytes(mode);
+    FrameSlots fs{c, cb};
     int cur = 0;
-    uint32_t i = 0;
+    uint32_t i = 0, idx = 0;
     int rc = LVLIP_OK;
     while (i < n && rc == LVLIP_OK) {
         Slot& s = c->slot[cur];
-        if ((rc = drain(c, s)) != LVLIP_OK) break;
+        if ((rc = fs.drain_slot(cur)) != LVLIP_OK) break;
         lvlip_frame_desc* hd = (lvlip_frame_desc*)s.h_desc;
         const uint32_t first = i;
-        const uint32_t k = n - i < fmax ? n - i : fmax;
+        const uint64_t pb = piece_bytes(c, idx++);
         uint64_t bytes = 0;
-        for (uint32_t q = 0; q < k; ++q) {
-            hd[q].offset = (uint64_t)(fr[first + q].head - h0);
-            hd[q].len = fr[first + q].len;
-            hd[q].reserved = 0;
-            bytes += fr[first + q].len;
+        uint32_t k = 0;
+        while (i < n && k < fmax && (k == 0 || bytes + fr[i].len <= pb)) {
+            bytes += fr[i].len;
+            ++k;
+            ++i;
         }
-        i += k;
+        write_descs(c, hd, fr + first, k, (uintptr_t)h0);
+        fs.first[cur] = first;
+        fs.count[cur] = k;
         rc = launch_frame_piece(c, s, mode, bytes ? bytes : 16, k, out + (size_t)first * ob, nullptr, d0);
         cur ^= 1;
     }
-    return finish_pieces(c, rc);
+    return fs.finish(rc, cur);
 }
 
 // Frames inside one LVLIP_REG_DMA region: a piece is a run of frames whose
 // byte span [lo, hi) (lo rounded down to 16, so every frame keeps its address
 // mod 16) fits the piece size; the copy engine reads the span from the region.
-int frames_dma(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out) {
+int frames_dma(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out, PieceDone* cb) {
     const uint32_t fmax = frames_per_piece(c, mode), ob = out_bytes(mode);
+    FrameSlots fs{c, cb};
     int cur = 0;
-    uint32_t i = 0;
+    uint32_t i = 0, idx = 0;
     int rc = LVLIP_OK;
     while (i < n && rc == LVLIP_OK) {
         Slot& s = c->slot[cur];
-        if ((rc = drain(c, s)) != LVLIP_OK) break;
+        if ((rc = fs.drain_slot(cur)) != LVLIP_OK) break;
         const uint32_t first = i;
         uintptr_t lo = ~(uintptr_t)0, hi = 0;
         uint32_t k = 0;
+        const uint64_t pb = piece_bytes(c, idx++);
         while (i < n && k < fmax) {
             const uintptr_t a = (uintptr_t)fr[i].head, e = a + fr[i].len;
             const uintptr_t nlo = (a & ~(uintptr_t)15) < lo ? (a & ~(uintptr_t)15) : lo;
             const uintptr_t nhi = e > hi ? e : hi;
-            if (align16(nhi) - nlo > (k ? c->piece : c->arena)) break;  // k = 0: fits (checked)
+            if (align16(nhi) - nlo > (k ? pb : c->arena)) break;  // k = 0: fits (checked)
             lo = nlo;
             hi = nhi;
             ++k;
             ++i;
         }
-        lvlip_frame_desc* hd = (lvlip_frame_desc*)s.h_desc;
-        for (uint32_t q = 0; q < k; ++q) {
-            hd[q].offset = (uint64_t)((uintptr_t)fr[first + q].head - lo);
-            hd[q].len = fr[first + q].len;
-            hd[q].reserved = 0;
-        }
+        write_descs(c, (lvlip_frame_desc*)s.h_desc, fr + first, k, lo);
+        fs.first[cur] = first;
+        fs.count[cur] = k;
         rc = launch_frame_piece(c, s, mode, hi - lo, k, out + (size_t)first * ob, (const uint8_t*)lo);
         cur ^= 1;
     }
-    return finish_pieces(c, rc);
+    return fs.finish(rc, cur);
 }
 
 // The region holding every frame, or nullptr.
@@ -239,10 +382,13 @@ const Region* one_region(const lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_
 
 // Runs the device step over all n frames; out gets n results (records or
 // verdicts).  Frames are only read.
-int frames_run(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out) {
+int frames_run_(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out,
+                PieceDone* cb) {
     DeviceGuard g(c->device);
     if (const Region* r = one_region(c, fr, n)) {
-        if (r->flags & LVLIP_REG_ZEROCOPY) return frames_zerocopy(c, *r, fr, n, mode, out);
+        // the header-only RX call reads ~64 B of each frame: in place, even
+        // from a DMA region (every region is mapped), rather than the spans
+        if ((r->flags & LVLIP_REG_ZEROCOPY) || mode == M_RX) return frames_zerocopy(c, *r, fr, n, mode, out, cb);
         // DMA only when the frames lie densely in the region (a slab of
         // frames): the spans are copied whole, gaps included
         uintptr_t lo = ~(uintptr_t)0, hi = 0;
@@ -255,28 +401,131 @@ int frames_run(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, u
             sum += fr[i].len;
             fits = fits && align16(fr[i].len + 15u) <= c->arena;
         }
-        if (fits && hi - lo <= 2 * sum + (1ull << 20)) return frames_dma(c, fr, n, mode, out);
+        if (fits && hi - lo <= 2 * sum + (1ull << 20)) return frames_dma(c, fr, n, mode, out, cb);
     }
-    // scattered: RX + L4 first reads each frame's total length (need_len),
-    // on the pool threads, prefetching ahead
-    uint32_t* len = nullptr;
-    if (mode == M_RX_L4) {
-        len = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
-        if (!len) return LVLIP_ENOMEM;
-        parallel_ranges(c, n, 4096, [=](uint64_t lo, uint64_t hi) {
-            for (uint64_t i = lo; i < hi; ++i) {
-                if (i + 16 < hi && fr[i + 16].head) __builtin_prefetch(fr[i + 16].head + kEth);
-                len[i] = need_len(mode, fr[i]);
+    // scattered: every frame's slot offset (a prefix sum over the frames'
+    // 16-B rounded need_len, in chunks on the pool threads); RX + L4 reads each
+    // frame's total length for it (need_len), prefetching ahead
+    constexpr uint32_t kChunk = 4096;
+    const uint32_t nch = (n + kChunk - 1) / kChunk;
+    const size_t lbytes = mode == M_RX_L4 ? align16(sizeof(uint32_t) * (size_t)n) : 0;
+    uint8_t* sc = (uint8_t*)scratch2(c, lbytes + 8 * ((size_t)n + 1) + 16 * (size_t)nch);
+    if (!sc) return LVLIP_ENOMEM;
+    uint32_t* len = mode == M_RX_L4 ? (uint32_t*)sc : nullptr;
+    uint64_t* pre = (uint64_t*)(sc + lbytes);
+    uint64_t* tot = pre + n + 1;  // per chunk: its slots' bytes, then the largest frame
+    const auto t = std::chrono::steady_clock::now();
+    parallel_ranges(c, nch, 1, [=](uint64_t lo, uint64_t hi) {
+        for (uint64_t j = lo; j < hi; ++j) {
+            const uint32_t a = (uint32_t)j * kChunk, b = a + kChunk < n ? a + kChunk : n;
+            uint64_t sum = 0, big = 0;
+            for (uint32_t i = a; i < b; ++i) {
+                uint32_t l;
+                if (len) {
+                    if (i + 16 < b && fr[i + 16].head) __builtin_prefetch(fr[i + 16].head + kEth);
+                    l = len[i] = need_len(mode, fr[i]);
+                } else {
+                    l = need_len(mode, fr[i]);
+                }
+                pre[i + 1] = sum += align16(l);  // within the chunk, for now
+                big = l > big ? l : big;
+            }
+            tot[2 * j] = sum;
+            tot[2 * j + 1] = big;
+        }
+    });
+    uint64_t base = 0;
+    bool fits = true;
+    for (uint32_t j = 0; j < nch; ++j) {
+        const uint64_t b = tot[2 * j];
+        tot[2 * j] = base;
+        base += b;
+        fits = fits && tot[2 * j + 1] <= c->arena;
+    }
+    pre[0] = 0;
+    parallel_ranges(c, nch, 1, [=](uint64_t lo, uint64_t hi) {
+        for (uint64_t j = lo; j < hi; ++j) {
+            const uint32_t a = (uint32_t)j * kChunk, b = a + kChunk < n ? a + kChunk : n;
+            for (uint32_t i = a; i < b; ++i) pre[i + 1] += tot[2 * j];
+        }
+    });
+    if (g_trace.on) g_trace.pass1 += Trace::ms(t);
+    if (!fits) return LVLIP_ERANGE;  // a frame larger than the arena
+    return frames_gather(c, fr, n, mode, out, len, pre, cb);
+}
+
+int frames_run(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out,
+               PieceDone* cb = nullptr) {
+    const char* e = getenv("LVLIP_FRAME_TRACE");
+    g_trace = Trace{};
+    g_trace.on = e && *e == '1';
+    g_trace.t0 = std::chrono::steady_clock::now();
+    const int rc = frames_run_(c, fr, n, mode, out, cb);
+    if (g_trace.on)
+        fprintf(stderr,
+                "lvlip frames: mode %d n %u pieces %u total %.3f ms pass1 %.3f gather %.3f wait %.3f apply %.3f\n",
+                mode, n, g_trace.pieces, Trace::ms(g_trace.t0), g_trace.pass1, g_trace.gather, g_trace.wait,
+                g_trace.apply);
+    return rc;
+}
+
+// TX: the records of each finished piece are stored into the caller's frames
+// while the later pieces run (the raw u16 stores of tcp_transmit_skb /
+// icmpv4_reply, L4 field, and ip_send_check, frame + 14 + 10), each frame's
+// old field values kept in undo[].  A piece holding a malformed frame (status
+// 0: not IPv4, short, ...) stops the applying, and the call then restores
+// every frame it wrote, so a malformed frame leaves the batch untouched as
+// include/lvlip_skb.h promises.
+constexpr uint64_t kApplied = 1ull << 48;  // record bit: this frame was written
+struct TxApply final : PieceDone {
+    lvlip_csum_ctx* c;
+    lvlip_frame* fr;
+    uint64_t* rec;
+    uint32_t* undo;
+    bool bad = false;
+    TxApply(lvlip_csum_ctx* c_, lvlip_frame* f, uint64_t* r, uint32_t* u) : c(c_), fr(f), rec(r), undo(u) {}
+    void done(uint32_t first, uint32_t k) override {
+        if (bad) return;
+        for (uint32_t i = first; i < first + k; ++i)
+            if (((rec[i] >> 40) & 0xffu) != 1u) {
+                bad = true;
+                return;
+            }
+        lvlip_frame* f = fr;
+        uint64_t* r = rec;
+        uint32_t* u = undo;
+        parallel_ranges(c, k, 2048, [=](uint64_t lo, uint64_t hi) {
+            for (uint64_t q = first + lo; q < first + hi; ++q) {
+                if (q + kPrefetch < first + hi) __builtin_prefetch(f[q + kPrefetch].head + kEth + 10, 1);
+                uint8_t* h = f[q].head;
+                const uint32_t o = (uint32_t)(r[q] >> 32) & 0xffu;
+                uint16_t oh, ol = 0;
+                memcpy(&oh, h + kEth + 10, 2);
+                if (o) memcpy(&ol, h + o, 2);
+                u[q] = oh | ((uint32_t)ol << 16);
+                const uint16_t hc = (uint16_t)r[q];
+                memcpy(h + kEth + 10, &hc, 2);
+                if (o) {
+                    const uint16_t lc = (uint16_t)(r[q] >> 16);
+                    memcpy(h + o, &lc, 2);
+                }
+                r[q] |= kApplied;
             }
         });
     }
-    int rc = LVLIP_OK;
-    for (uint32_t i = 0; i < n && rc == LVLIP_OK; ++i)
-        if ((uint64_t)(len ? len[i] : need_len(mode, fr[i])) > c->arena) rc = LVLIP_ERANGE;
-    if (rc == LVLIP_OK) rc = frames_gather(c, fr, n, mode, out, len);
-    free(len);
-    return rc;
-}
+    // the frames written so far back to their old bytes (the L4 field first:
+    // it may overlap nothing else, but restore in reverse order of writing)
+    void undo_all(uint32_t n) {
+        for (uint32_t q = 0; q < n; ++q) {
+            if (!(rec[q] & kApplied)) continue;
+            uint8_t* h = fr[q].head;
+            const uint32_t o = (uint32_t)(rec[q] >> 32) & 0xffu;
+            const uint16_t oh = (uint16_t)undo[q], ol = (uint16_t)(undo[q] >> 16);
+            if (o) memcpy(h + o, &ol, 2);
+            memcpy(h + kEth + 10, &oh, 2);
+        }
+    }
+};
 
 }  // namespace
 
@@ -297,32 +546,15 @@ int lvlip_tx_checksum(lvlip_csum_ctx* ctx, lvlip_frame* frames, uint32_t n) {
     if (ctx->frame_hostplan) return lvlip_tx_checksum_hostplan(ctx, frames, n);
     for (uint32_t i = 0; i < n; ++i)  // what needs no frame byte (the rest: the device's status)
         if (!frames[i].head || frames[i].len < kEth + 20u) return LVLIP_EINVAL;
-    uint64_t* rec = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)n);
+    // the context's scratch: n records, then n undo words
+    uint64_t* rec = (uint64_t*)scratch(ctx, 12 * (size_t)n);
     if (!rec) return LVLIP_ENOMEM;
-    int rc = frames_run(ctx, frames, n, M_TX, (uint8_t*)rec);
-    // tx_frame_ok of every frame (status 1) before any frame is written
-    for (uint32_t i = 0; i < n && rc == LVLIP_OK; ++i)
-        if (((rec[i] >> 40) & 0xffu) != 1u) rc = LVLIP_EINVAL;
-    if (rc == LVLIP_OK) {
-        // the raw u16 stores of tcp_transmit_skb / icmpv4_reply (L4 field) and
-        // ip_send_check (header field, frame + 14 + 10)
-        lvlip_frame* fr = frames;
-        parallel_ranges(ctx, n, 8192, [=](uint64_t lo, uint64_t hi) {
-            for (uint64_t i = lo; i < hi; ++i) {
-                if (i + 16 < hi) __builtin_prefetch(fr[i + 16].head + kEth + 10, 1);
-                const uint64_t r = rec[i];
-                uint8_t* h = fr[i].head;
-                const uint16_t hc = (uint16_t)r;
-                memcpy(h + kEth + 10, &hc, 2);
-                const uint32_t o = (uint32_t)(r >> 32) & 0xffu;
-                if (o) {
-                    const uint16_t lc = (uint16_t)(r >> 16);
-                    memcpy(h + o, &lc, 2);
-                }
-            }
-        });
-    }
-    free(rec);
+    uint32_t* undo = (uint32_t*)(rec + n);
+    memset(rec, 0, 8 * (size_t)n);  // undo_all reads the applied bit of every record, drained or not
+    TxApply ap(ctx, frames, rec, undo);
+    int rc = frames_run(ctx, frames, n, M_TX, (uint8_t*)rec, &ap);
+    if (rc == LVLIP_OK && ap.bad) rc = LVLIP_EINVAL;
+    if (rc != LVLIP_OK) ap.undo_all(n);  // a malformed frame (or a failure): every frame as it was
     return rc;
 }
 

@@ -13,7 +13,10 @@
 #   e2e[:WL]              the bench line with its host-resident (PCIe-inclusive) rates and small-batch latency
 #   frames                the mixed bench line with its device frame-call diag (TX fill, RX verify)
 #   txstore               scripts/lab_tx_store.py (TX field-store A/B + probes)
+#   fhost[:R]             scripts/lab_frames_host.py (host frame pipeline: ramps, threads; R rounds)
 #   rehearse:N            bench.py --gpus N self-launched over gloo, the ranks sharing the one GPU
+#   rehearse_strong:N     the same with --workload tcp1500x64m (64M packets split over the N ranks)
+#   rehearse_root:N       the same with --origin root (the batch scattered from rank 0's GPU first)
 #   wb                    scripts/lab_wb.py (field-store forms paired with the RX + L4 sweep)
 #   txpmc                 FETCH_SIZE / WRITE_SIZE passes of the TX variants
 #   modes:K               K processes of scripts/lab_modes.py (mixed line modes)
@@ -49,7 +52,11 @@ for step in "$@"; do
     e2e:*) wl=${step#e2e:}; run "e2e_$wl" 300 python bench.py --workload "$wl" --e2e ;;
     frames) run frames 300 python bench.py --workload mixed --frames ;;
     rehearse:*) n=${step#rehearse:}; run "rehearse_n$n" 300 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --steps 50 --warmup 10 ;;
+    rehearse_strong:*) n=${step#rehearse_strong:}; run "rehearse_strong_n$n" 400 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --workload tcp1500x64m --steps 20 --warmup 5 ;;
+    rehearse_root:*) n=${step#rehearse_root:}; run "rehearse_root_n$n" 300 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --origin root --steps 50 --warmup 10 ;;
     wb) run wb 400 python scripts/lab_wb.py "gpurun_out/${TAG}_wb.json" 5 ;;
+    fhost) run fhost 500 python scripts/lab_frames_host.py "gpurun_out/${TAG}_frames_host.json" 3 ;;
+    fhost:*) r=${step#fhost:}; run fhost 500 python scripts/lab_frames_host.py "gpurun_out/${TAG}_frames_host.json" "$r" ;;
     txstore) run txstore 400 python scripts/lab_tx_store.py "gpurun_out/${TAG}_tx_store.json" 7 ;;
     txpmc)
       for v in ${TXPMC_VARIANTS:-tx_product tx_nt tx_sec32 rx_l4}; do

@@ -26,6 +26,13 @@ end of a socketpair and whatever the stack transmits shows up on the other end.
 OUT.json: {"replies": per frame the bytes the stack wrote in response (hex,
 several frames joined by "|"), or null; "verdicts": the batch's verdicts (null
 for unbatched)}.
+
+On oracle/_ref/libref_rxq.so (ip_rcv's header checksum at src/ip_input.c:38
+gated on the batch verdict, oracle/ref_rxq.c) the batched modes mark every
+accepted skb's IPv4 header before ip_rcv, so :38 takes the batch's result
+instead of summing it again; OUT.json then also holds "cpu_header_sums" (the
+header sums ip_rcv ran on the CPU) and "batch_header_sums" (the ones the
+batch answered).
 """
 import ctypes
 import json
@@ -83,6 +90,11 @@ def main(frames_path: str, out_path: str, so_path: str, mode: str):
         ctypes.memmove(skb.contents.data, fr, len(fr))
         skbs.append(skb)
     replies, verdicts = [], None
+    gated = hasattr(lib, "lvlip_rxq_accept")
+    if gated:
+        lib.lvlip_rxq_accept.argtypes = [ctypes.c_void_p]
+        lib.lvlip_rxq_computed.restype = ctypes.c_ulong
+        lib.lvlip_rxq_skipped.restype = ctypes.c_ulong
     if mode == "unbatched":
         for skb, fr in zip(skbs, frames):
             netdev_receive(skb, fr)
@@ -112,14 +124,22 @@ def main(frames_path: str, out_path: str, so_path: str, mode: str):
         import lvlip  # noqa: F811 (constants only on the oracle path)
         for skb, fr, vd in zip(skbs, frames, verdicts):
             if vd == lvlip.RX_OK:
-                lib.ip_rcv(skb)  # the checks are taken; ip_rcv repeats them (same outcome)
+                if gated:  # ip_hdr(skb) = skb->head + ETH_HDR_LEN (include/ip.h:47-50)
+                    assert lib.lvlip_rxq_accept(skb.contents.head + 14) == 0
+                # the checks are taken; ip_rcv repeats them (same outcome), and
+                # on libref_rxq.so skips the header sum (:38) the batch made
+                lib.ip_rcv(skb)
             elif vd == lvlip.RX_NOT_IP:
                 netdev_receive(skb, fr)
             else:
                 lib.free_skb(skb)  # ip_rcv's drop_pkt
             replies.append(sent())
+    out = {"replies": replies, "verdicts": verdicts}
+    if gated:
+        out["cpu_header_sums"] = int(lib.lvlip_rxq_computed())
+        out["batch_header_sums"] = int(lib.lvlip_rxq_skipped())
     with open(out_path, "w") as f:
-        json.dump({"replies": replies, "verdicts": verdicts}, f)
+        json.dump(out, f)
 
 
 if __name__ == "__main__":

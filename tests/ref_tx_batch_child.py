@@ -78,7 +78,6 @@ def main(req_path: str, out_path: str, so_path: str, mode: str):
 
     batched = mode != "unbatched"
     batches, deferred = [], []
-    ctx = None
     if batched:
         import lvlip
 
@@ -86,15 +85,19 @@ def main(req_path: str, out_path: str, so_path: str, mode: str):
         lib.lvlip_txq_frames.argtypes = [ctypes.POINTER(lvlip.Frame), ctypes.c_int]
         lib.lvlip_txq_fill_gpu.argtypes = [ctypes.c_void_p]
         lib.lvlip_txq_deferred.restype = ctypes.c_ulong
-        if mode == "gpu":
-            ctx = lvlip.Context(0)
+    ctxs = []
 
     def flush():
         if not batched:
             return
         n = lib.lvlip_txq_len()
         if mode == "gpu":
-            rc = lib.lvlip_txq_fill_gpu(ctx._h)
+            # created at the first flush, after the TCP sends: the HIP
+            # runtime's start-up draws from rand(), which generate_iss
+            # (src/tcp.c:153) must see unseeded as in the unbatched run
+            if not ctxs:
+                ctxs.append(lvlip.Context(0))
+            rc = lib.lvlip_txq_fill_gpu(ctxs[0]._h)
             if rc != n:
                 raise SystemExit(f"lvlip_txq_fill_gpu: {rc} (queue {n})")
         else:
@@ -141,8 +144,8 @@ def main(req_path: str, out_path: str, so_path: str, mode: str):
     th.join(timeout=30)
     if th.is_alive():
         raise SystemExit("reader did not see the end marker")
-    if ctx is not None:
-        ctx.close()
+    for c in ctxs:
+        c.close()
     with open(out_path, "w") as f:
         json.dump({"frames": got, "batches": batches, "deferred": deferred}, f)
 

@@ -171,6 +171,28 @@ def test_bench_self_launch_two_ranks_dry_run():
     assert line["cpu_baseline"] is None
 
 
+@pytest.mark.parametrize("extra", [[], ["--workload", "tcp1500x64m"], ["--origin", "root"]],
+                         ids=["weak", "strong64m", "origin_root"])
+def test_bench_self_launch_eight_ranks_dry_run(extra):
+    """The three 8-rank commands the driver's scaling run can issue (VERDICT
+    r04 Next #3): the default weak line, the 64M x 1500 B strong config
+    (BASELINE configs[4]) and the root-origin scatter, each `bench.py --gpus
+    8` starting its own eight ranks (gloo rehearsal on the CPU, --dry-run):
+    one line naming eight ranks, in order, for the whole job."""
+    out = _bench(["--gpus", "8", "--dry-run", "--steps", "2", "--warmup", "1", "--settle-ms", "0"] + extra,
+                 timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["dry_run"] is True and line["n_gpus"] == 8
+    d = line["dist"]
+    assert d["world_size"] == 8 and d["backend"] == "gloo" and d["launcher"] == "bench.py"
+    assert [r["rank"] for r in d["ranks"]] == list(range(8))
+    if "tcp1500x64m" in extra:
+        assert line["scaling"] == "strong"
+
+
 def test_bench_world_mismatch_fails():
     """WORLD_SIZE from a launcher that disagrees with --gpus is an error."""
     out = _bench(["--gpus", "3", "--dry-run", "--steps", "1", "--warmup", "0"],

@@ -31,12 +31,15 @@ ARP = (b"\xff" * 6 + ref_rx_cases.TAP_MAC + b"\x08\x06" + bytes.fromhex("0001080
 needs_ref = pytest.mark.skipif(not os.path.exists(ref_rx_cases.REF_SO), reason="oracle/_ref/libref.so not built")
 
 
-def _run(frames, mode):
+REF_RXQ = os.path.join(os.path.dirname(ref_rx_cases.REF_SO), "libref_rxq.so")
+
+
+def _run(frames, mode, so=ref_rx_cases.REF_SO):
     with tempfile.TemporaryDirectory() as d:
         fin, fout = os.path.join(d, "f.json"), os.path.join(d, "o.json")
         with open(fin, "w") as f:
             json.dump([bytes(x).hex() for x in frames], f)
-        r = subprocess.run([sys.executable, CHILD, fin, fout, ref_rx_cases.REF_SO, mode],
+        r = subprocess.run([sys.executable, CHILD, fin, fout, so, mode],
                            stdin=subprocess.DEVNULL, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-3000:]
         with open(fout) as f:
@@ -107,3 +110,38 @@ def test_batched_rx_with_l4_verify_drops_corrupted_icmp():
             assert r is not None and g is None and v == lvlip.RX_BAD_L4
         else:
             assert g == r, k
+
+
+def _gated(mode):
+    """The composition on libref_rxq.so, where ip_rcv's header checksum
+    (src/ip_input.c:38) takes the batch's verdict for accepted frames
+    (INTEGRATION.md §2b's one-line change, made at link level): per accepted
+    frame, the CPU header sums the batch removes."""
+    frames, kinds = _frames(84, 12)
+    ref = _run(frames, "unbatched", REF_RXQ)
+    got = _run(frames, mode, REF_RXQ)
+    assert got["replies"] == ref["replies"]
+    accepted = sum(v == lvlip.RX_OK for v in got["verdicts"])
+    # unbatched: ip_rcv sums the header of every IPv4 frame that passes the
+    # version / ihl / TTL checks (ok, options, bad checksum, unknown protocol,
+    # bad ICMP checksum: 5 of the 8 kinds)
+    reaching = sum(k in ("ok", "ok_options", "ip_csum", "proto", "icmp_csum") for k in kinds)
+    assert ref["cpu_header_sums"] == reaching and ref["batch_header_sums"] == 0
+    # batched: the rejected frames never reach ip_rcv, the accepted ones take
+    # the batch's result: no header is summed on the CPU
+    assert got["cpu_header_sums"] == 0 and got["batch_header_sums"] == accepted > 0
+    return ref, got
+
+
+@pytest.mark.skipif(not os.path.exists(REF_RXQ), reason="oracle/_ref/libref_rxq.so not built")
+def test_gated_ip_rcv_takes_batch_verdicts_oracle():
+    """CPU: the gated composition with the oracle's verdicts."""
+    _gated("oracle")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_RXQ), reason="oracle/_ref/libref_rxq.so not built")
+def test_gated_ip_rcv_takes_batch_verdicts_gpu():
+    """GPU: one lvlip_rx_verify_skb_list, then ip_rcv with :38 answered by the
+    batch; replies identical to the unbatched stack, zero CPU header sums."""
+    _gated("batched")

@@ -199,12 +199,13 @@ def test_host_frames_every_source_matches_oracle(ctx, source):
 
 @pytest.mark.parametrize("source", SOURCES)
 def test_host_tx_malformed_untouched_every_source(ctx, source):
-    """One malformed frame (version 6) among 5 000: LVLIP_EINVAL and every
-    frame byte unchanged, whichever source the frames come from (the device
-    fills records, the host stores nothing until all are well formed)."""
-    fr = workloads.frames(5000, seed=86, max_l4=1460)
+    """One malformed frame (version 6) among 20 000, in a late piece: the
+    host has already stored the fields of the earlier pieces (the apply runs
+    per piece) and must restore them: LVLIP_EINVAL and every frame byte
+    unchanged, whichever source the frames come from."""
+    fr = workloads.frames(20000, seed=86, max_l4=1460)
     views, buf = _frames_in(source, fr, seed=87)
-    views[2500][14] = 0x65
+    views[17500][14] = 0x65
     before = [bytes(v) for v in views]
     _registered(ctx, source, buf)
     try:
@@ -240,7 +241,7 @@ def test_rx_verify_skb_buffers_longer_than_frames(ctx):
         got = ctx.rx_verify(bufs, flags)
         want = np.array([skb_oracle.rx_verdict(bytes(b), flags) for b in bufs], dtype=np.uint8)
         assert np.array_equal(got, want), (flags, np.nonzero(got != want)[0][:5])
-    assert (got == lvlip.RX_OK).sum() > 4000
+    assert (got == lvlip.RX_OK).sum() > 3500
 
 
 def test_host_frames_hostplan_ab_agrees(monkeypatch):
