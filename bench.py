@@ -706,6 +706,7 @@ def frames_dev(lvlip, torch, dev):
     v = lvlip.rx_verify_dev(base, fdt, 0, stream=stream)
     torch.cuda.synchronize(dev)
     res["rx_header_all_ok"] = bool((v == lvlip.RX_OK).all())
+    res["echo_reply"] = echo_reply_timing(lvlip, torch, base, fd, fdt, pay, stream)
     # the same frames from host memory through the host API (PCIe-inclusive),
     # on a 512K-frame prefix
     nh = min(n, 1 << 19)
@@ -714,6 +715,36 @@ def frames_dev(lvlip, torch, dev):
     res["host"] = frames_host(lvlip, dev, host, fd[:nh], int(pay["len"][:nh].sum()))
     log("device-resident frames", res)
     return res
+
+
+def echo_reply_timing(lvlip, torch, base, fd, fdt, pay, stream, reps=7):
+    """f4 on the mixed frames in HBM: every ICMP frame made an
+    echo request (type 8, code 0; its checksum field is whatever the TX fill
+    left, so flags 0's field is the RFC 1624 one, not verified), then
+    lvlip_icmp_echo_reply_dev with flags 0 (one 64-B sector per frame) and
+    with LVLIP_ECHO_FULL (each lane sums its whole message), HIP events around
+    each launch alone; the request bytes are restored before every launch.
+    GB/s counts the ICMP messages' bytes."""
+    icmp = pay["start_sum"] == 0
+    t_off = torch.from_numpy((fd["offset"][icmp] + 34).astype(np.int64)).to(base.device)
+    msg_bytes = int(pay["len"][icmp].sum())
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    out = {"icmp_frames": int(icmp.sum()), "icmp_bytes": msg_bytes}
+    for name, flags in (("flags0", 0), ("full", lvlip.ECHO_FULL)):
+        ms = []
+        for _ in range(reps):
+            base[t_off] = 8
+            base[t_off + 1] = 0
+            torch.cuda.synchronize()
+            e0.record(stream)
+            st = lvlip.icmp_echo_reply_dev(base, fdt, stream=stream, flags=flags)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms.append(e0.elapsed_time(e1))
+        med = sorted(ms)[len(ms) // 2]
+        out[name] = {"ms": round(med, 4), "GBps": round(msg_bytes / med / 1e6, 1),
+                     "replies": int((st.cpu() != 0).sum())}
+    return out
 
 
 def frames_host(lvlip, dev, host, fd, l4_bytes):

@@ -13,8 +13,14 @@
  *      context), and
  *   2. does the same by hand: lvlip_partition_bytes, then one pthread per
  *      context calling lvlip_csum_batch_host_flat on its part,
- * and checks every result of both against the per-call drop-in checksum()
- * (src/utils.c:40-55 semantics).  Prints "multi_gpu ok ..." and exits 0.
+ *   3. shards it device-resident, the way the headline metric shards
+ *      (BASELINE configs[4], bench.py --gpus N): part k's span copied once
+ *      into device k % lvlip_device_count()'s HBM (HIP runtime C API), then
+ *      one lvlip_csum_batch_dev per part on its own device, the parts'
+ *      threads running at once, no exchange between them,
+ * and checks every result of all three against the per-call drop-in
+ * checksum() (src/utils.c:40-55 semantics).  Prints "multi_gpu ok ..." and
+ * exits 0.
  *
  *   make -C examples && examples/build/multi_gpu [frames] [contexts]
  */
@@ -23,6 +29,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <hip/hip_runtime_api.h>
 
 #include "lvlip_csum.h"
 
@@ -51,6 +59,66 @@ static void *run_part(void *arg)
 {
     struct part *p = (struct part *)arg;
     p->rc = p->n ? lvlip_csum_batch_host_flat(p->ctx, p->base, p->base_bytes, p->d, p->n, p->out) : 0;
+    return NULL;
+}
+
+/* 3.: one shard in HBM.  The part's descriptors keep their offsets from the
+ * span's first byte rounded down to 16 (lvlip_csum_batch_dev wants a 16-B
+ * aligned base, and every packet keeps its address mod 16). */
+struct dev_part {
+    int device;
+    const uint8_t *base;
+    const lvlip_csum_desc *d;
+    uint32_t n;
+    uint16_t *out;
+    int rc;
+    char err[160];
+};
+
+static void *run_dev_part(void *arg)
+{
+    struct dev_part *p = (struct dev_part *)arg;
+    p->rc = 0;
+    if (!p->n)
+        return NULL;
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t i = 0; i < p->n; i++) {
+        const uint64_t e = p->d[i].offset + (uint64_t)(p->d[i].len > 0 ? p->d[i].len : 0);
+        lo = p->d[i].offset < lo ? p->d[i].offset : lo;
+        hi = e > hi ? e : hi;
+    }
+    lo &= ~15ull;
+    const size_t span = (size_t)((hi - lo + 15u) & ~15ull);
+    lvlip_csum_desc *dd = malloc((size_t)p->n * sizeof *dd);
+    void *dbase = NULL, *ddesc = NULL, *dout = NULL;
+    hipError_t e = hipSetDevice(p->device);
+    if (e == hipSuccess) e = hipMalloc(&dbase, span ? span : 16);
+    if (e == hipSuccess) e = hipMalloc(&ddesc, (size_t)p->n * sizeof *dd);
+    if (e == hipSuccess) e = hipMalloc(&dout, (size_t)p->n * sizeof(uint16_t));
+    if (e == hipSuccess && dd) {
+        for (uint32_t i = 0; i < p->n; i++) {
+            dd[i] = p->d[i];
+            dd[i].offset -= lo;
+        }
+        /* the span's tail past hi is read as whole 16-B chunks: copy the
+         * bytes that exist, the rest of the last chunk stays unset */
+        e = hipMemcpy(dbase, p->base + lo, (size_t)(hi - lo), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(ddesc, dd, (size_t)p->n * sizeof *dd, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess || !dd) {
+        snprintf(p->err, sizeof p->err, "device %d: %s", p->device, dd ? hipGetErrorString(e) : "out of memory");
+        p->rc = -1;
+    } else if ((p->rc = lvlip_csum_batch_dev(dbase, ddesc, p->n, dout, NULL)) != 0) {
+        snprintf(p->err, sizeof p->err, "lvlip_csum_batch_dev: %s", lvlip_strerror(p->rc));
+    } else if ((e = hipDeviceSynchronize()) != hipSuccess ||
+               (e = hipMemcpy(p->out, dout, (size_t)p->n * sizeof(uint16_t), hipMemcpyDeviceToHost)) != hipSuccess) {
+        snprintf(p->err, sizeof p->err, "device %d: %s", p->device, hipGetErrorString(e));
+        p->rc = -1;
+    }
+    (void)hipFree(dbase);
+    (void)hipFree(ddesc);
+    (void)hipFree(dout);
+    free(dd);
     return NULL;
 }
 
@@ -130,18 +198,38 @@ int main(int argc, char **argv)
             return 1;
         }
     }
-    uint32_t bad1 = 0, bad2 = 0;
+    /* 3. device-resident shards: one lvlip_csum_batch_dev per device */
+    uint16_t *got3 = malloc(n * sizeof *got3);
+    struct dev_part dparts[MAX_CTX];
+    for (uint32_t c = 0; c < k; c++) {
+        dparts[c] = (struct dev_part){(int)(c % (uint32_t)ndev), base, d + cuts[c], cuts[c + 1] - cuts[c],
+                                      got3 + cuts[c], 0, ""};
+        if (pthread_create(&th[c], NULL, run_dev_part, &dparts[c]) != 0) {
+            fprintf(stderr, "multi_gpu: pthread_create failed for device part %u\n", c);
+            return 1;
+        }
+    }
+    for (uint32_t c = 0; c < k; c++) {
+        pthread_join(th[c], NULL);
+        if (dparts[c].rc) {
+            fprintf(stderr, "multi_gpu: device part %u: %s\n", c, dparts[c].err);
+            return 1;
+        }
+    }
+    uint32_t bad1 = 0, bad2 = 0, bad3 = 0;
     for (uint32_t i = 0; i < n; i++) {
         bad1 += got1[i] != want[i];
         bad2 += got2[i] != want[i];
+        bad3 += got3[i] != want[i];
     }
     for (uint32_t c = 0; c < k; c++)
         lvlip_csum_ctx_destroy(ctx[c]);
-    if (bad1 || bad2) {
-        fprintf(stderr, "multi_gpu: %u / %u of %u checksums differ from checksum()\n", bad1, bad2, n);
+    if (bad1 || bad2 || bad3) {
+        fprintf(stderr, "multi_gpu: %u / %u / %u of %u checksums differ from checksum()\n", bad1, bad2, bad3, n);
         return 1;
     }
-    printf("multi_gpu ok: %u descriptors over %u contexts on %d device(s), parts", n, k, ndev);
+    printf("multi_gpu ok: %u descriptors over %u contexts on %d device(s) (host-resident and "
+           "device-resident shards), parts", n, k, ndev);
     for (uint32_t c = 0; c < k; c++)
         printf(" %u", cuts[c + 1] - cuts[c]);
     printf("\n");
@@ -150,5 +238,6 @@ int main(int argc, char **argv)
     free(want);
     free(got1);
     free(got2);
+    free(got3);
     return 0;
 }

@@ -39,12 +39,16 @@ extern "C" {
  * declared in this header are exported. */
 #pragma GCC visibility push(default)
 
-/* 2 (round 4): ids 1, 2, 4, 6, 7 and 9 are no longer accepted by
- * lvlip_csum_batch_dev_ex (LVLIP_EINVAL: A/B variants, liblvlip_lab.so), and
+/* 2 (round 4): what changed from 1 for a caller of lvlip_csum_batch_dev_ex:
  * FLAT's unroll takes only 2, 4 or 8 (the group-order bits << 8 and the
- * 512-descriptor tile bit 1 << 10 are refused); added Group 4
+ * 512-descriptor tile bit 1 << 10, A/B shapes, are now LVLIP_EINVAL here and
+ * live in liblvlip_lab.so); the kernel ids the A/B library retired in round 4
+ * (2, 4, 5, 11, 12, 14, 15) are LVLIP_EINVAL in both libraries (the product
+ * already refused every id but 0, 3, 8 and 10 in ABI 1).  Added: Group 4
  * (lvlip_partition_bytes, lvlip_csum_batch_host_flat_multi) and
- * lvlip_icmp_echo_reply_dev_ex (include/lvlip_skb.h).  INTEGRATION.md §5. */
+ * lvlip_icmp_echo_reply_dev_ex (include/lvlip_skb.h).  INTEGRATION.md §5.
+ * Round 5 changed no entry point: the host frame calls' implementation moved
+ * to the device (include/lvlip_skb.h), with the same results. */
 #define LVLIP_CSUM_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------- */
@@ -259,7 +263,9 @@ int lvlip_partition_bytes(const lvlip_csum_desc *d, uint32_t n, uint32_t parts,
  * must not use them concurrently), and must be distinct (a context is owned
  * by one thread at a time: the same pointer twice is LVLIP_EINVAL).  Returns
  * 0 or the first part's LVLIP_E* in part order (results of failed parts are
- * not meaningful). */
+ * not meaningful); lvlip_last_hip_error() on the calling thread then holds
+ * that part's HIP message.  A part whose thread cannot be started runs on the
+ * calling thread. */
 int lvlip_csum_batch_host_flat_multi(lvlip_csum_ctx *const *ctxs, uint32_t nctx,
                                      const void *base, size_t base_bytes,
                                      const lvlip_csum_desc *d, uint32_t n,

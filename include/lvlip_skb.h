@@ -10,9 +10,13 @@
  * Ethernet header, the IPv4 header is at head + 14 (ip_hdr(), include/ip.h:47-50)
  * and the TCP/ICMP header right after it (tcp_hdr(), include/tcp.h:224-227).
  *
- * Each call is plan -> one batch -> apply.  The plan and apply steps are
- * exported too: they are plain host logic (no GPU) and are what the CPU tests
- * exercise.
+ * The device parses every frame (the same kernels as the _dev calls below):
+ * the host moves whole frames to the GPU (a gather into a pinned arena, or,
+ * for frames inside a registered region, DMA of its spans or in-place reads),
+ * and gets back one verdict (RX) or one record of the two fields (TX) per
+ * frame.  The plan and apply steps below are the same decisions as plain host
+ * logic (no GPU): the CPU tests exercise them, and round 4's host-plan path
+ * (LVLIP_FRAME_PATH=hostplan, for A/B) batches through them.
  */
 #ifndef LVLIP_SKB_H
 #define LVLIP_SKB_H
@@ -190,7 +194,11 @@ int lvlip_icmp_echo_reply_dev(void *base, const lvlip_frame_desc *frames, uint32
 /* flags of lvlip_icmp_echo_reply_dev_ex */
 #define LVLIP_ECHO_FULL 0x1u /* sum every request's message (one lane per frame)
                                 and write icmpv4_reply's field exactly: for
-                                any request, verified or not; status 2 */
+                                any request, verified or not; status 2.  Costs
+                                a full read of each message by its one lane
+                                (serial 16-B loads), where flags 0 reads one
+                                64-B sector per frame (DESIGN.md §9 times
+                                both) */
 
 /* lvlip_icmp_echo_reply_dev with flags: 0 is lvlip_icmp_echo_reply_dev (the
  * precondition above holds); LVLIP_ECHO_FULL computes the reply's field as

@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -31,8 +32,11 @@ constexpr uint64_t kPieceMax = 32ull << 20;  // measured: DESIGN.md §5
 namespace lvlip_ctx {
 
 int fail(lvlip_csum_ctx* c, hipError_t e, const char* what, int code) {
-    if (c) snprintf(c->err, sizeof c->err, "%s: %s", what, hipGetErrorString(e));
-    fprintf(stderr, "lvlip_csum: %s: %s\n", what, hipGetErrorString(e));
+    char msg[256];
+    snprintf(msg, sizeof msg, "%s: %s", what, hipGetErrorString(e));
+    if (c) snprintf(c->err, sizeof c->err, "%s", msg);
+    lvlip_set_last_hip_error(msg);  // what lvlip_last_hip_error() returns on this thread
+    fprintf(stderr, "lvlip_csum: %s\n", msg);
     return code;
 }
 
@@ -448,29 +452,44 @@ int lvlip_csum_batch_host_flat_multi(lvlip_csum_ctx* const* ctxs, uint32_t nctx,
     std::vector<uint32_t> cuts;
     std::vector<int> rcs;
     std::vector<std::thread> th;
+    std::vector<std::string> errs;  // each part's lvlip_last_hip_error() (thread-local)
     try {  // no exception leaves the C ABI
         cuts.resize(nctx + 1u);
         rcs.assign(nctx, LVLIP_OK);
+        errs.resize(nctx);
         th.reserve(nctx);
     } catch (...) {
         return LVLIP_ENOMEM;
     }
     int rc = lvlip_partition_bytes(d, n, nctx, cuts.data());
     if (rc != LVLIP_OK) return rc;
-    auto part = [&](uint32_t k) {
+    auto part = [&](uint32_t k) noexcept {
         const uint32_t lo = cuts[k], hi = cuts[k + 1];
         if (hi > lo) rcs[k] = lvlip_csum_batch_host_flat(ctxs[k], base, base_bytes, d + lo, hi - lo, out + lo);
+        if (rcs[k] != LVLIP_OK) {
+            try {
+                errs[k] = lvlip_last_hip_error();
+            } catch (...) {
+            }
+        }
     };
+    // parts 1.. on threads of their own; a part whose thread cannot be
+    // started runs on the calling thread after part 0 (a thread shortage
+    // costs the overlap, not the call)
+    uint32_t started = 1;
     try {
-        for (uint32_t k = 1; k < nctx; ++k) th.emplace_back(part, k);
+        for (; started < nctx; ++started) th.emplace_back(part, started);
     } catch (...) {
-        rc = LVLIP_ENOMEM;  // no thread: the parts already started still finish below
     }
-    part(0);  // part 0 on the calling thread
+    part(0);
+    for (uint32_t k = started; k < nctx; ++k) part(k);
     for (auto& t : th) t.join();
-    if (rc != LVLIP_OK) return rc;
     for (uint32_t k = 0; k < nctx; ++k)
-        if (rcs[k] != LVLIP_OK) return rcs[k];
+        if (rcs[k] != LVLIP_OK) {
+            // the failing part's HIP message, on the caller's thread
+            lvlip_set_last_hip_error(errs[k].c_str());
+            return rcs[k];
+        }
     return LVLIP_OK;
 }
 

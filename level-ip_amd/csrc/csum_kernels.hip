@@ -552,6 +552,11 @@ int lvlip_abi_version(void) { return LVLIP_CSUM_ABI_VERSION; }
 
 const char* lvlip_last_hip_error(void) { return g_last_err; }
 
+// Hidden: the host context (csum_ctx.cpp, frames_host.cpp) records its HIP
+// failures here too, and Group 4 hands a worker thread's message to the
+// calling thread.
+void lvlip_set_last_hip_error(const char* msg) { snprintf(g_last_err, sizeof g_last_err, "%s", msg ? msg : ""); }
+
 int lvlip_device_count(void) {
     int c = 0;
     if (hipGetDeviceCount(&c) != hipSuccess) return 0;

@@ -667,7 +667,7 @@ __attribute__((visibility("default"))) int lvlip_lab_window_stamps(const void* b
     return hipGetLastError() == hipSuccess ? (int)(grid * wpb) : LVLIP_EHIP;
 }
 
-// lvlip_csum_batch_dev_ex's contract for the lab kernel ids (1, 2, 3, 4, 5, 9, 11).
+// lvlip_csum_batch_dev_ex's contract for the lab kernel ids (1, 3, 9, 13).
 __attribute__((visibility("default"))) int lvlip_lab_batch_dev_ex(const void* base,
                                                                   const lvlip_csum_desc* descs, uint32_t n,
                                                                   uint16_t* out, void* stream,
