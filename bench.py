@@ -747,6 +747,34 @@ def echo_reply_timing(lvlip, torch, base, fd, fdt, pay, stream, reps=7):
     return out
 
 
+def cpu_header_check(lvlip, host, fd, budget_s=0.3):
+    """What ip_rcv's header check costs on one host core (src/ip_input.c:38:
+    checksum(ih, ihl * 4, 0) per received frame), to set beside the RX batch's
+    host-path cost per frame: the n frames' 20-B IPv4 headers (frame + 14) of
+    the host slab, level-ip's own checksum() (oracle/_ref, -O0 as built) and
+    the product's per-call drop-in, ns per header (the CPU-baseline leg)."""
+    import pyoracle  # test infrastructure: a reported CPU baseline only
+
+    d = np.zeros(fd.size, dtype=lvlip.DESC_DTYPE)
+    d["offset"] = fd["offset"] + 14
+    d["len"] = 20
+    res = {"headers": int(fd.size)}
+    kinds = [("dropin_ns", {"csum_fn": lvlip.lib().checksum})]
+    if pyoracle.reflib() is not None:
+        kinds.insert(0, ("reference_O0_ns", {"use_reference": True}))
+    # over the whole slab every header is a cache miss; in the stack ip_rcv
+    # sums a header tun_read has just written: the first 2 048 frames' headers
+    # again and again (in cache) give that case
+    for tag, dd in (("", d), ("_cached", d[:2048])):
+        for name, kw in kinds:
+            reps, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < budget_s:
+                pyoracle.batch(host, dd, threads=1, **kw)
+                reps += 1
+            res[name.replace("_ns", tag + "_ns")] = round((time.perf_counter() - t0) / reps / dd.size * 1e9, 2)
+    return res
+
+
 def frames_host(lvlip, dev, host, fd, l4_bytes):
     """The host frame calls (include/lvlip_skb.h lvlip_tx_checksum,
     lvlip_rx_verify) on n frames in host memory, PCIe included, wall time per
@@ -832,6 +860,7 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
                 run(ctx, arr, tag)
         finally:
             del os.environ[k]
+    out["cpu_header_check"] = cpu_header_check(lvlip, host, fd)
     # the frames the TX calls filled are what the HBM frames hold after
     # tx_fill (same bytes, same fill): spot-check the slab against the scatter
     for i in range(0, n, max(1, n // 997)):

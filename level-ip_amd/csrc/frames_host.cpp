@@ -396,17 +396,19 @@ int frames_run_(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, 
         // 1.2 as DMA'd spans)
         // DMA only when the frames lie densely in the region (a slab of
         // frames): the spans are copied whole, gaps included
-        uintptr_t lo = ~(uintptr_t)0, hi = 0;
-        uint64_t sum = 0;
-        bool fits = true;
-        for (uint32_t i = 0; i < n; ++i) {
-            const uintptr_t a = (uintptr_t)fr[i].head;
-            lo = a < lo ? a : lo;
-            hi = a + fr[i].len > hi ? a + fr[i].len : hi;
-            sum += fr[i].len;
-            fits = fits && align16(fr[i].len + 15u) <= c->arena;
+        if (mode != M_RX) {
+            uintptr_t lo = ~(uintptr_t)0, hi = 0;
+            uint64_t sum = 0;
+            bool fits = true;
+            for (uint32_t i = 0; i < n; ++i) {
+                const uintptr_t a = (uintptr_t)fr[i].head;
+                lo = a < lo ? a : lo;
+                hi = a + fr[i].len > hi ? a + fr[i].len : hi;
+                sum += fr[i].len;
+                fits = fits && align16(fr[i].len + 15u) <= c->arena;
+            }
+            if (fits && hi - lo <= 2 * sum + (1ull << 20)) return frames_dma(c, fr, n, mode, out, cb);
         }
-        if (mode != M_RX && fits && hi - lo <= 2 * sum + (1ull << 20)) return frames_dma(c, fr, n, mode, out, cb);
     }
     // scattered: every frame's slot offset (a prefix sum over the frames'
     // 16-B rounded need_len, in chunks on the pool threads); RX + L4 reads each
