@@ -664,14 +664,19 @@ int lvlip_icmp_echo_reply_dev_ex(void* base, const lvlip_frame_desc* frames, uin
     if (n == 0) return LVLIP_OK;
     if (!base || !frames || ((uintptr_t)base & 15u)) return LVLIP_EINVAL;
     hipStream_t s = (hipStream_t)stream;
+    if (flags & LVLIP_ECHO_FULL) {
+        // the whole messages: the flat sweep with a frame source (round 5;
+        // one lane per frame summing its message alone ran 3-4x slower,
+        // DESIGN.md §9)
+        if (n > kMaxFrames * 2u) return LVLIP_EINVAL;
+        const int rc = lvlip::launch_frames_flat<lvlip::FR_ECHO, 8, 2>(base, frames, n, status, s, false);
+        if (rc == LVLIP_EHIP) return hip_fail(hipGetLastError(), "k_flat2 echo");
+        return rc;
+    }
     for (uint32_t f0 = 0; f0 < n;) {
         const uint32_t m = n - f0 < kLaunchMax ? n - f0 : kLaunchMax;
-        if (flags & LVLIP_ECHO_FULL)
-            hipLaunchKernelGGL(lvlip::k_echo_reply<true>, dim3((m + 255u) / 256u), dim3(256), 0, s, (uint8_t*)base,
-                               frames + f0, m, status ? status + f0 : nullptr);
-        else
-            hipLaunchKernelGGL(lvlip::k_echo_reply<false>, dim3((m + 255u) / 256u), dim3(256), 0, s,
-                               (uint8_t*)base, frames + f0, m, status ? status + f0 : nullptr);
+        hipLaunchKernelGGL(lvlip::k_echo_reply<false>, dim3((m + 255u) / 256u), dim3(256), 0, s,
+                           (uint8_t*)base, frames + f0, m, status ? status + f0 : nullptr);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "k_echo_reply");
         f0 += m;

@@ -59,7 +59,10 @@ constexpr uint32_t FR_HAS_L4 = 0x200;   // plan word: the TCP/ICMP entry exists
 // be well formed).  Record (u64): bits 0-15 the IPv4 header field, 16-31 the
 // TCP/ICMP field, 32-39 the TCP/ICMP field's offset from the frame's first
 // byte (0 = the frame has no such field), 40-47 status (1 filled, 0 malformed).
-enum { FR_TX = 0, FR_RX = 1, FR_RX_L4 = 2, FR_TX_REC = 3 };
+// FR_ECHO: f4's LVLIP_ECHO_FULL (lvlip_icmp_echo_reply_dev_ex): one entry per
+// frame, the ICMP message of an echo request, seeded so that its result is
+// icmpv4_reply's field; put() writes the reply's type and field.
+enum { FR_TX = 0, FR_RX = 1, FR_RX_L4 = 2, FR_TX_REC = 3, FR_ECHO = 4 };
 constexpr bool fr_is_tx(int mode) { return mode == FR_TX || mode == FR_TX_REC; }
 
 __device__ __forceinline__ uint32_t fr_be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
@@ -261,7 +264,7 @@ struct FrameSrc {
     uint8_t* out8;                   // RX: verdict[], TX: status[] (may be null)
     bool nt_store = false;           // TX: nontemporal field stores (the launcher's default)
     uint64_t* rec = nullptr;         // FR_TX_REC: one record per frame
-    static constexpr uint32_t SLOTS = MODE == FR_RX ? 1u : 2u;
+    static constexpr uint32_t SLOTS = (MODE == FR_RX || MODE == FR_ECHO) ? 1u : 2u;
     // the frame descriptor of entry i (k_flat2's PFA prefetch: 16 B, like a
     // batch descriptor)
     __device__ __forceinline__ const lvlip_frame_desc* desc_ptr(uint32_t i) const { return frames + i / SLOTS; }
@@ -358,6 +361,37 @@ struct FrameSrc {
         }
     }
 
+    // the checks of lvlip_icmp_echo_reply_fill (skb_batch.c): an IPv4 ICMP echo
+    // request (type 8, code 0) whose message lies inside the frame -> its
+    // message as the entry, seeded with -(0x0008 + HC): the reply's message is
+    // the request's with word 0 (type 8, code 0: LE 0x0008) and word 1 (the
+    // field HC) zeroed, so its u32 word sum is W - 0x0008 - HC, and the
+    // entry's result is icmpv4_reply's field (src/icmpv4.c:45-47) for any
+    // request, verified or not.  Plan word: 1 = a request.
+    __device__ __forceinline__ void parse_echo(const lvlip_frame_desc& fd, const uint8_t* h, const FrWin& x,
+                                               lvlip_csum_desc& d0, uint32_t& w) const {
+        if (fd.len < FR_ETH + 20u) return;
+        const uint32_t ver = x.b(14) >> 4, ihl = x.b(14) & 0x0fu, iplen = x.be16(16);
+        const uint32_t l4 = FR_ETH + ihl * 4u;
+        if (ver != 4u || ihl < 5u || x.b(23) != 1u || iplen < ihl * 4u + 4u || fd.len < FR_ETH + iplen) return;
+        // type, code and checksum from the window when it holds them (ihl <= 9)
+        uint32_t type, code, hc;
+        if (l4 + 4u <= 56u) {
+            const uint32_t q = (ihl == 5u) ? x.le32(34) : (ihl == 6u) ? x.le32(38) : (ihl == 7u) ? x.le32(42)
+                             : (ihl == 8u) ? x.le32(46) : x.le32(50);
+            type = q & 0xffu;
+            code = (q >> 8) & 0xffu;
+            hc = q >> 16;
+        } else {
+            type = h[l4];
+            code = h[l4 + 1u];
+            hc = fr_le16(h + l4 + 2u);
+        }
+        if (type != 8u || code != 0u) return;
+        d0 = fr_mk(fd.offset + l4, iplen - ihl * 4u, 0u - 0x0008u - hc);
+        w = 1u;
+    }
+
     __device__ __forceinline__ lvlip_csum_desc get(uint32_t i, uint32_t& w, uint4* win = nullptr,
                                                    uint64_t* wa = nullptr) const {
         // the descriptor's two words in flight together (the compiler would
@@ -382,6 +416,8 @@ struct FrameSrc {
         w = 0;
         if (fr_is_tx(MODE))
             parse_tx(fd, h, x, d0, d1, w);
+        else if (MODE == FR_ECHO)
+            parse_echo(fd, h, x, d0, w);
         else
             parse_rx(fd, x, d0, d1, w);
         if (win) {
@@ -402,6 +438,23 @@ struct FrameSrc {
     __device__ __forceinline__ void put(uint32_t i, uint16_t c, uint32_t w, bool valid,
                                         uint64_t addr) const {
         const uint32_t f = i / SLOTS;
+        if constexpr (MODE == FR_ECHO) {
+            // the reply: ICMP type 0 (ICMP_V4_REPLY, src/icmpv4.c:45) and the
+            // field, stored raw, at the message's first bytes (inside the
+            // entry: a neighbouring tile reads them only in an edge chunk,
+            // whose out-of-entry bytes it subtracts as loaded)
+            if (!valid) return;
+            uint32_t st = 0;
+            if (w & 1u) {
+                uint8_t* p = wbase + (addr - reinterpret_cast<uint64_t>(base));
+                p[0] = 0u;
+                p[2] = (uint8_t)c;
+                p[3] = (uint8_t)(c >> 8);
+                st = 2u;
+            }
+            if (out8) out8[f] = (uint8_t)st;
+            return;
+        }
         if constexpr (MODE == FR_TX_REC) {
             // the header lane (slot 2f) writes the frame's record with the L4
             // lane's result (every lane runs the shuffle)
