@@ -17,8 +17,9 @@
 //               scan.  Also the frame calls' kernel (flat_src.h).
 //   k_lane    : up to 32 B (IPv4 headers alone): a few lanes per packet.
 //   k_rx_hdr  : the header-only RX frame call, one lane per frame (csum_dev.h).
-//   k_echo_reply : f4, the RFC 1624 echo reply of verified requests (or, with
-//               LVLIP_ECHO_FULL, icmpv4_reply's full sum), one lane per frame.
+//   k_echo_reply : f4, the RFC 1624 echo reply of verified requests, one lane
+//               per frame (LVLIP_ECHO_FULL, icmpv4_reply's full sum, runs on
+//               k_flat2 with a frame source).
 // The A/B variants still under study (k_stream, k_wflat, k_flat2's other
 // shapes and occupancies, the frame calls' store forms) live in
 // liblvlip_lab.so (lab_kernels.hip); the ones rejected by >= 3 % were pruned
@@ -187,29 +188,10 @@ __device__ __forceinline__ uint32_t oc_add16(uint32_t a, uint32_t b) {
     return (t & 0xffffu) + (t >> 16);
 }
 
-// FULL (LVLIP_ECHO_FULL): the lane sums the whole request message W (16-B
-// aligned chunk loads, bytes outside it masked) and writes icmpv4_reply's own
-// result, finish(0, W - 0x0008 - HC): the reply's message is the request's
-// with word 0 (type 8, code 0 = LE word 0x0008) and word 1 (the field)
-// zeroed, and u32 sums differ by exactly those words.  No precondition.
-__device__ __forceinline__ uint32_t msg_word_sum(const uint8_t* m, uint32_t len) {
-    const uint64_t a = reinterpret_cast<uint64_t>(m);
-    const uint64_t a0 = a & ~15ull;
-    const uint32_t lo = (uint32_t)(a & 15ull);
-    const uint32_t span = lo + len;
-    const uint32_t nch = (span + 15u) >> 4;
-    const uint32_t lastv = span - 16u * (nch - 1u);
-    const bool odd = a & 1ull;
-    uint32_t acc = 0;
-    for (uint32_t c = 0; c < nch; ++c) {
-        uint4 v = load_global(a0 + 16ull * c);
-        v = mask_chunk(v, c == 0u ? (int)lo : 0, c + 1u == nch ? (int)lastv : 16);
-        acc += odd ? chunk_words<true>(v) : chunk_words<false>(v);
-    }
-    return acc;
-}
-
-template <bool FULL>
+// LVLIP_ECHO_FULL (icmpv4_reply's full sum for any request) is not this
+// kernel: it runs on the flat sweep with a frame source (FrameSrc<FR_ECHO>,
+// flat_src.h; round 5: 0.23 against 0.51 ms for one lane per frame summing
+// its message alone, 1M requests).
 __global__ __launch_bounds__(256) void k_echo_reply(uint8_t* __restrict__ base,
                                                     const lvlip_frame_desc* __restrict__ frames,
                                                     uint32_t n, uint8_t* __restrict__ status) {
@@ -247,10 +229,7 @@ __global__ __launch_bounds__(256) void k_echo_reply(uint8_t* __restrict__ base,
                 const uint32_t S = hc == 0xffffu ? 0xffffu : (~hc & 0xffffu);
                 const uint32_t S1 = oc_add16(S, 0xffffu - 0x0008u);
                 uint32_t field;
-                if (FULL) {
-                    field = finish(0u, msg_word_sum(h + l4, icmp_len) - 0x0008u - hc);
-                    st = 2u;
-                } else if (S1 != 0xffffu) {
+                if (S1 != 0xffffu) {
                     field = ~S1 & 0xffffu;
                     st = 1u;
                 } else {
@@ -675,7 +654,7 @@ int lvlip_icmp_echo_reply_dev_ex(void* base, const lvlip_frame_desc* frames, uin
     }
     for (uint32_t f0 = 0; f0 < n;) {
         const uint32_t m = n - f0 < kLaunchMax ? n - f0 : kLaunchMax;
-        hipLaunchKernelGGL(lvlip::k_echo_reply<false>, dim3((m + 255u) / 256u), dim3(256), 0, s,
+        hipLaunchKernelGGL(lvlip::k_echo_reply, dim3((m + 255u) / 256u), dim3(256), 0, s,
                            (uint8_t*)base, frames + f0, m, status ? status + f0 : nullptr);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "k_echo_reply");
