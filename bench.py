@@ -931,21 +931,41 @@ def latency(lvlip, torch, dev):
 
 
 def e2e(lvlip, b, base):
-    """Host-resident batch, PCIe-inclusive: pinned gather + H2D + kernel + D2H;
-    then the f3 paths over the same buffer registered in place (copy engine
-    straight from it; kernel reading it over PCIe)."""
+    """Host-resident batch, PCIe-inclusive: pinned gather + H2D + kernel + D2H
+    (one flat buffer, lvlip_csum_batch_host_flat); the f3 paths over the same
+    buffer registered in place (copy engine straight from it; kernel reading it
+    over PCIe); and the same packets as an iov array, one pointer each
+    (lvlip_csum_batch_host: a gather per packet)."""
+    import ctypes
+
     host = np.ascontiguousarray(base.cpu().numpy()[: b.nbytes])
+    # the same packets as an iov array (lvlip_csum_batch_host: one pointer per
+    # packet, as the reference's call sites hold skb payloads)
+    iov = np.zeros(b.n, dtype=[("ptr", "<u8"), ("len", "<i4"), ("start_sum", "<u4")])
+    assert iov.dtype.itemsize == ctypes.sizeof(lvlip.Iov)
+    iov["ptr"] = host.ctypes.data + b.descs["offset"]
+    iov["len"] = b.descs["len"]
+    iov["start_sum"] = b.descs["start_sum"]
+    iov_p = ctypes.cast(iov.ctypes.data, ctypes.POINTER(lvlip.Iov))
+    out = np.empty(b.n, np.uint16)
+    lib = lvlip.lib()
     res = {}
     for name, flags in (("flat", None), ("registered_dma", lvlip.REG_DMA),
-                        ("registered_zerocopy", lvlip.REG_ZEROCOPY)):
+                        ("registered_zerocopy", lvlip.REG_ZEROCOPY), ("iov", None)):
         with lvlip.Context(base.device.index or 0, arena_bytes=256 << 20) as ctx:
             if flags is not None:
                 ctx.register(host, flags)
-            ctx.batch_host_flat(host, b.descs)
+            if name == "iov":
+                def call():
+                    assert lib.lvlip_csum_batch_host(ctx._h, iov_p, b.n, out.ctypes.data) == 0
+            else:
+                def call():
+                    ctx.batch_host_flat(host, b.descs)
+            call()
             t0 = time.perf_counter()
             reps = 3
             for _ in range(reps):
-                ctx.batch_host_flat(host, b.descs)
+                call()
             dt = (time.perf_counter() - t0) / reps
         res[f"{name}_GBps"] = round(b.algo_bytes / dt / 1e9, 2)
     log("e2e host-resident GB/s", res)

@@ -354,14 +354,20 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
             ++k;
             ++i;
         }
-        // ... then gather the bytes, packets split over the host threads
+        // ... then gather the bytes, packets split over the host threads,
+        // nontemporal stores (copy_nt), the next packets prefetched
         {
             uint8_t* dst = s.h_bytes;
             const lvlip_csum_desc* hd = s.h_desc;
             const lvlip_csum_iov* src = pkts + first;
             parallel_ranges(c, k, 1024, [=](uint64_t lo, uint64_t hi) {
-                for (uint64_t q = lo; q < hi; ++q)
-                    if (hd[q].len > 0) memcpy(dst + hd[q].offset, src[q].ptr, (size_t)hd[q].len);
+                for (uint64_t q = lo; q < hi; ++q) {
+                    if (q + 8 < hi && hd[q + 8].len > 0)
+                        for (int32_t l = 0; l < hd[q + 8].len; l += 64)
+                            __builtin_prefetch((const uint8_t*)src[q + 8].ptr + l);
+                    if (hd[q].len > 0) copy_nt(dst + hd[q].offset, (const uint8_t*)src[q].ptr, (uint64_t)hd[q].len);
+                }
+                _mm_sfence();
             });
         }
         rc = launch_piece(c, s, off ? off : 16, k, out + first);
@@ -421,10 +427,14 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
             // exactly `span` and let the kernel's 16-B tail read the arena.
             from = b + lo16;
         } else if (span) {
+            // the span in 64-B blocks over the threads, nontemporal stores
             uint8_t* dst = s.h_bytes;
             const uint8_t* src = b + lo16;
-            parallel_ranges(c, span, 512u << 10, [=](uint64_t lo, uint64_t hi) {
-                memcpy(dst + lo, src + lo, hi - lo);
+            const uint64_t nblk = (span + 63) / 64;
+            parallel_ranges(c, nblk, 8192, [=](uint64_t lo, uint64_t hi) {
+                const uint64_t e = hi * 64 < span ? hi * 64 : span;
+                copy_nt(dst + lo * 64, src + lo * 64, e - lo * 64);
+                _mm_sfence();
             });
         }
         for (uint32_t q = 0; q < k; ++q) {

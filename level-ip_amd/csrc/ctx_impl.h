@@ -12,9 +12,11 @@
 // piece k-1's H2D copy, kernel and D2H copy run on the other slot's stream.
 #pragma once
 
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <string.h>
 
 #include <vector>
 
@@ -105,6 +107,34 @@ struct DeviceGuard {
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 };
+
+// len bytes from src (any alignment) to the 16-B aligned dst with nontemporal
+// 16-B stores: the gathers into the pinned arena, which the copy engine (or
+// the kernel, over PCIe) reads next.  Stores that bypass the CPU caches leave
+// no dirty lines for those reads to snoop and need no read for ownership of
+// the arena's lines (measured).  The last partial chunk goes
+// through a zeroed 16-B temporary: nothing past src + len is read, and the
+// chunk's bytes past len become zero.  The caller fences (_mm_sfence) before
+// the data is handed to the device.
+inline void copy_nt(uint8_t* dst, const uint8_t* src, uint64_t len) {
+    uint64_t k = 0;
+    for (; k + 64 <= len; k += 64) {
+        const __m128i a = _mm_loadu_si128((const __m128i*)(src + k));
+        const __m128i b = _mm_loadu_si128((const __m128i*)(src + k + 16));
+        const __m128i c = _mm_loadu_si128((const __m128i*)(src + k + 32));
+        const __m128i d = _mm_loadu_si128((const __m128i*)(src + k + 48));
+        _mm_stream_si128((__m128i*)(dst + k), a);
+        _mm_stream_si128((__m128i*)(dst + k + 16), b);
+        _mm_stream_si128((__m128i*)(dst + k + 32), c);
+        _mm_stream_si128((__m128i*)(dst + k + 48), d);
+    }
+    for (; k + 16 <= len; k += 16) _mm_stream_si128((__m128i*)(dst + k), _mm_loadu_si128((const __m128i*)(src + k)));
+    if (k < len) {
+        alignas(16) uint8_t t[16] = {0};
+        memcpy(t, src + k, (size_t)(len - k));
+        _mm_stream_si128((__m128i*)(dst + k), _mm_load_si128((const __m128i*)t));
+    }
+}
 
 // Runs fn(lo, hi) over [0, n) split into up to c->threads contiguous ranges of
 // at least min_per_thread.  The gather into pinned memory is host-memory-

@@ -35,8 +35,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <emmintrin.h>
-
 #include <algorithm>
 #include <chrono>
 
@@ -104,33 +102,6 @@ void* scratch2(lvlip_csum_ctx* c, size_t bytes) {
         c->frame_scratch2_bytes = c->frame_scratch2 ? bytes : 0;
     }
     return c->frame_scratch2;
-}
-
-// One frame into its 16-B aligned arena slot with nontemporal 16-B stores.
-// The copy engine reads the arena next: stores that bypass the CPU caches
-// leave no dirty lines for its reads to snoop, and need no read-for-ownership
-// of the slot's lines (measured).  The last partial chunk goes
-// through a zeroed 16-B temporary (nothing past the frame's end is read; the
-// slot's padding bytes become zero).  The caller fences (_mm_sfence) before
-// the copy engine is started.
-inline void copy_frame_nt(uint8_t* dst, const uint8_t* src, uint32_t len) {
-    uint32_t k = 0;
-    for (; k + 64 <= len; k += 64) {
-        const __m128i a = _mm_loadu_si128((const __m128i*)(src + k));
-        const __m128i b = _mm_loadu_si128((const __m128i*)(src + k + 16));
-        const __m128i c = _mm_loadu_si128((const __m128i*)(src + k + 32));
-        const __m128i d = _mm_loadu_si128((const __m128i*)(src + k + 48));
-        _mm_stream_si128((__m128i*)(dst + k), a);
-        _mm_stream_si128((__m128i*)(dst + k + 16), b);
-        _mm_stream_si128((__m128i*)(dst + k + 32), c);
-        _mm_stream_si128((__m128i*)(dst + k + 48), d);
-    }
-    for (; k + 16 <= len; k += 16) _mm_stream_si128((__m128i*)(dst + k), _mm_loadu_si128((const __m128i*)(src + k)));
-    if (k < len) {
-        alignas(16) uint8_t t[16] = {0};
-        memcpy(t, src + k, len - k);
-        _mm_stream_si128((__m128i*)(dst + k), _mm_load_si128((const __m128i*)t));
-    }
 }
 
 // Frames per piece: the slot's descriptor array and its result buffer.
@@ -274,7 +245,7 @@ int frames_gather(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode
                     hd[q].offset = pf[q] - pf[0];
                     hd[q].len = l;
                     hd[q].reserved = 0;
-                    if (l) copy_frame_nt(dst + hd[q].offset, src[q].head, l);
+                    if (l) copy_nt(dst + hd[q].offset, src[q].head, l);
                 }
                 _mm_sfence();  // the nontemporal stores land before the copy engine reads
             });

@@ -179,6 +179,41 @@ static void slab(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed, uint32_t reg) {
     free(s);
 }
 
+// The packet batches of the same context (csum_ctx.cpp): scattered exact-size
+// packets at every alignment (lvlip_csum_batch_host: a gather per packet) and
+// one flat buffer ending at its last packet's last byte (a gather per span).
+static void packets(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed) {
+    Rng r{seed};
+    std::vector<uint8_t*> mem(n);
+    std::vector<lvlip_csum_iov> iov(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const int32_t len = (r() % 97u == 0) ? -(int32_t)(r() % 5u) : (int32_t)(r() % 3001u);
+        const uint32_t off = r() % 16u;
+        const size_t bytes = off + (len > 0 ? (size_t)len : 0) + (len <= 0);
+        mem[i] = (uint8_t*)malloc(bytes);
+        for (size_t b = 0; b < bytes; ++b) mem[i][b] = (uint8_t)r();
+        iov[i] = {mem[i] + off, len, r()};
+    }
+    std::vector<uint16_t> out(n, 0);
+    CHECK(lvlip_csum_batch_host(ctx, iov.data(), n, out.data()) == LVLIP_OK, "batch_host");
+    for (uint32_t i = 0; i < n; ++i)
+        CHECK(out[i] == oracle_checksum(iov[i].ptr, iov[i].len, (int)iov[i].start_sum), "batch_host %u", i);
+    for (auto* p : mem) free(p);
+    std::vector<lvlip_csum_desc> d(n);
+    uint64_t pos = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        pos += r() % 40u;
+        d[i] = {pos, (int32_t)(r() % 1601u), r()};
+        pos += (uint64_t)d[i].len;
+    }
+    uint8_t* base = (uint8_t*)malloc(pos ? pos : 1);
+    for (uint64_t b = 0; b < pos; ++b) base[b] = (uint8_t)r();
+    CHECK(lvlip_csum_batch_host_flat(ctx, base, pos, d.data(), n, out.data()) == LVLIP_OK, "batch_host_flat");
+    for (uint32_t i = 0; i < n; ++i)
+        CHECK(out[i] == oracle_checksum(base + d[i].offset, d[i].len, (int)d[i].start_sum), "flat %u", i);
+    free(base);
+}
+
 int main() {
     for (int direct = 0; direct < 2; ++direct) {
         // direct: pieces read in place; else through the H2D / D2H copies
@@ -186,6 +221,7 @@ int main() {
         lvlip_csum_ctx* ctx = nullptr;
         CHECK(lvlip_csum_ctx_create(&ctx, 0, 1u << 20) == LVLIP_OK, "ctx_create");
         scattered(ctx, 12000, 1 + direct);
+        packets(ctx, 12000, 7 + direct);
         slab(ctx, 12000, 3 + direct, LVLIP_REG_DMA);
         slab(ctx, 6000, 5 + direct, LVLIP_REG_ZEROCOPY);
         CHECK(lvlip_csum_ctx_destroy(ctx) == LVLIP_OK, "destroy");
