@@ -214,6 +214,10 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         const char* e = getenv("LVLIP_FRAME_PATH");
         c->frame_hostplan = e && strcmp(e, "hostplan") == 0;
     }
+    {
+        const char* e = getenv("LVLIP_FRAME_TRACE");
+        c->frame_trace = e && *e == '1';
+    }
     // descriptors per piece: one per 64 B of arena (a piece of smaller packets
     // simply ends at this count; the next piece takes the rest)
     c->max_desc = (uint32_t)(arena_bytes / 64 < 4096 ? 4096 : arena_bytes / 64);

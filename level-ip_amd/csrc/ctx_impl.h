@@ -77,6 +77,7 @@ struct lvlip_csum_ctx {
     void* frame_scratch2 = nullptr;
     size_t frame_scratch2_bytes = 0;
     int frame_hostplan = 0;   // LVLIP_FRAME_PATH=hostplan: round 4's host frame path (A/B)
+    int frame_trace = 0;      // LVLIP_FRAME_TRACE=1: per-step host times on stderr
     lvlip_ctx::Slot slot[lvlip_ctx::kSlots];
     std::vector<lvlip_ctx::Region> regions;
     lvlip::GatherPool pool;

@@ -120,8 +120,9 @@ inline uint64_t piece_bytes(const lvlip_csum_ctx* c, uint32_t idx) {
     return r < c->piece ? r : c->piece;
 }
 
-// LVLIP_FRAME_TRACE=1: one line per call on stderr with the host's time in
-// each step (diagnostics for the pipeline's balance; off by default).
+// LVLIP_FRAME_TRACE=1 (read when the context is made): one line per call on
+// stderr with the host's time in each step (diagnostics for the pipeline's
+// balance; off by default).
 struct Trace {
     bool on = false;
     std::chrono::steady_clock::time_point t0;
@@ -434,9 +435,8 @@ int frames_run_(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, 
 
 int frames_run(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out,
                PieceDone* cb = nullptr) {
-    const char* e = getenv("LVLIP_FRAME_TRACE");
     g_trace = Trace{};
-    g_trace.on = e && *e == '1';
+    g_trace.on = c->frame_trace != 0;
     g_trace.t0 = std::chrono::steady_clock::now();
     const int rc = frames_run_(c, fr, n, mode, out, cb);
     if (g_trace.on)
