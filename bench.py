@@ -789,8 +789,8 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
       zerocopy   the slab registered LVLIP_REG_ZEROCOPY (kernel reads in place)
       hostplan   the slab through round 4's path (LVLIP_FRAME_PATH=hostplan:
                  the CPU plans every frame, two gathered pieces per frame)
-      scattered_t16  scattered with 16 gather threads (LVLIP_GATHER_THREADS;
-                 the default is 8)
+      scattered_t8  scattered with 8 gather threads (LVLIP_GATHER_THREADS;
+                 the default is min(hardware threads, 16), round 4's was 8)
     GB/s counts the checksummed bytes (20 B header + L4 per frame) as the
     device lines do; frame_GBps counts the frames' bytes (what crosses PCIe)."""
     import ctypes
@@ -852,7 +852,7 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
             finally:
                 ctx.unregister(host)
     for env, tag, arr in (("LVLIP_FRAME_PATH=hostplan", "hostplan", keep_slab[1]),
-                          ("LVLIP_GATHER_THREADS=16", "scattered_t16", keep_scat[1])):
+                          ("LVLIP_GATHER_THREADS=8", "scattered_t8", keep_scat[1])):
         k, v = env.split("=")
         os.environ[k] = v
         try:
