@@ -787,8 +787,6 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
                  random order over an n x 1616 B buffer (the gather path)
       dma        the slab registered LVLIP_REG_DMA (copy engine reads spans)
       zerocopy   the slab registered LVLIP_REG_ZEROCOPY (kernel reads in place)
-      hostplan   the slab through round 4's path (LVLIP_FRAME_PATH=hostplan:
-                 the CPU plans every frame, two gathered pieces per frame)
       scattered_t8  scattered with 8 gather threads (LVLIP_GATHER_THREADS;
                  the default is min(hardware threads, 16), round 4's was 8)
     GB/s counts the checksummed bytes (20 B header + L4 per frame) as the
@@ -851,8 +849,7 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
                 run(ctx, keep_slab[1], tag)
             finally:
                 ctx.unregister(host)
-    for env, tag, arr in (("LVLIP_FRAME_PATH=hostplan", "hostplan", keep_slab[1]),
-                          ("LVLIP_GATHER_THREADS=8", "scattered_t8", keep_scat[1])):
+    for env, tag, arr in (("LVLIP_GATHER_THREADS=8", "scattered_t8", keep_scat[1]),):
         k, v = env.split("=")
         os.environ[k] = v
         try:

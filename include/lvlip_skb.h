@@ -15,8 +15,9 @@
  * for frames inside a registered region, DMA of its spans or in-place reads),
  * and gets back one verdict (RX) or one record of the two fields (TX) per
  * frame.  The plan and apply steps below are the same decisions as plain host
- * logic (no GPU): the CPU tests exercise them, and round 4's host-plan path
- * (LVLIP_FRAME_PATH=hostplan, for A/B) batches through them.
+ * logic (no GPU): the CPU tests and the sanitizer harness exercise them.
+ * (Round 4's host frame path batched the planned pieces through
+ * lvlip_csum_batch_host; round 5 retired it, slower from every source.)
  */
 #ifndef LVLIP_SKB_H
 #define LVLIP_SKB_H

@@ -208,12 +208,6 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         const long long v = e ? atoll(e) : 0;
         c->first_piece = v > 0 ? align16((uint64_t)v) : (4ull << 20);
     }
-    // LVLIP_FRAME_PATH=hostplan: the host frame calls plan on the CPU (round
-    // 4's path, skb_batch.c) instead of parsing on the device (frames_host.cpp)
-    {
-        const char* e = getenv("LVLIP_FRAME_PATH");
-        c->frame_hostplan = e && strcmp(e, "hostplan") == 0;
-    }
     {
         const char* e = getenv("LVLIP_FRAME_TRACE");
         c->frame_trace = e && *e == '1';

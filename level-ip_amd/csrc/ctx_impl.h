@@ -76,7 +76,6 @@ struct lvlip_csum_ctx {
     size_t frame_scratch_bytes = 0;
     void* frame_scratch2 = nullptr;
     size_t frame_scratch2_bytes = 0;
-    int frame_hostplan = 0;   // LVLIP_FRAME_PATH=hostplan: round 4's host frame path (A/B)
     int frame_trace = 0;      // LVLIP_FRAME_TRACE=1: per-step host times on stderr
     lvlip_ctx::Slot slot[lvlip_ctx::kSlots];
     std::vector<lvlip_ctx::Region> regions;

@@ -24,10 +24,6 @@
 // to be well formed, so a malformed frame still leaves the whole batch
 // untouched (include/lvlip_skb.h).  Pieces are double-buffered over the two
 // slots as in csum_ctx.cpp.
-//
-// LVLIP_FRAME_PATH=hostplan (read at context creation) runs round 4's path
-// instead, which plans every frame on the CPU and gathers the two checksummed
-// pieces per frame through lvlip_csum_batch_host (skb_batch.c), for A/B.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -39,13 +35,6 @@
 #include <chrono>
 
 #include "ctx_impl.h"
-
-extern "C" {
-// skb_batch.c: round 4's host-plan path (hidden)
-int lvlip_rx_verify_hostplan(lvlip_csum_ctx* ctx, const lvlip_frame* frames, uint32_t n, uint32_t flags,
-                             uint8_t* verdict);
-int lvlip_tx_checksum_hostplan(lvlip_csum_ctx* ctx, lvlip_frame* frames, uint32_t n);
-}
 
 namespace {
 
@@ -514,14 +503,12 @@ int lvlip_rx_verify(lvlip_csum_ctx* ctx, const lvlip_frame* frames, uint32_t n, 
     // two checksums per frame at most: n as the _dev call
     if (!ctx || (n && (!frames || !verdict)) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
-    if (ctx->frame_hostplan) return lvlip_rx_verify_hostplan(ctx, frames, n, flags, verdict);
     return frames_run(ctx, frames, n, (flags & LVLIP_RX_VERIFY_L4) ? M_RX_L4 : M_RX, verdict);
 }
 
 int lvlip_tx_checksum(lvlip_csum_ctx* ctx, lvlip_frame* frames, uint32_t n) {
     if (!ctx || (n && !frames) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
-    if (ctx->frame_hostplan) return lvlip_tx_checksum_hostplan(ctx, frames, n);
     for (uint32_t i = 0; i < n; ++i)  // what needs no frame byte (the rest: the device's status)
         if (!frames[i].head || frames[i].len < kEth + 20u) return LVLIP_EINVAL;
     // the context's scratch: n records, then n undo words

@@ -2,17 +2,15 @@
  * skb_batch.c — f1/f2 of SURVEY.md §8f: batch-and-dispatch over level-ip frames.
  * See include/lvlip_skb.h for the contract; every decision cites the reference
  * line it mirrors.  Host logic only: the exported plan/apply steps, f4 on the
- * host, the skb-queue walkers, and round 4's host-plan frame path (the
- * checksums as one GPU batch through lvlip_csum_batch_host), which
- * frames_host.cpp keeps as an A/B under LVLIP_FRAME_PATH=hostplan.  The
- * product's host frame calls parse on the device (frames_host.cpp).
+ * host and the skb-queue walkers.  The host frame calls themselves parse on
+ * the device (frames_host.cpp); round 4's path, which planned every frame
+ * here and batched the planned pieces, was retired in round 5 once the device
+ * parse measured faster from every source.
  */
-#include <pthread.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
-#include <unistd.h>
 
 #include "lvlip_skb.h"
 
@@ -51,61 +49,6 @@ uint32_t lvlip_pseudo_sum_rfc(uint32_t saddr, uint32_t daddr, uint8_t proto, uin
      * no carry is lost: sum < 6 * 0xffff, folded by the checksum's final fold */
     return (saddr & 0xffffu) + (saddr >> 16) + (daddr & 0xffffu) + (daddr >> 16) +
            bswap16((uint16_t)proto) + bswap16(len);
-}
-
-/* A batch's host steps (plan, apply) run over contiguous frame ranges on up to
- * PAR_MAX threads: each range is DRAM-latency bound on its own, and the ranges
- * are independent.  Range t covers frames [n*t/T, n*(t+1)/T). */
-#define PAR_MAX 16u
-#define PAR_MIN_FRAMES 8192u
-
-typedef struct par_job {
-    void (*fn)(void *arg, uint32_t t, uint32_t lo, uint32_t hi);
-    void *arg;
-    uint32_t t, lo, hi;
-} par_job;
-
-static void *par_main(void *p)
-{
-    par_job *j = (par_job *)p;
-    j->fn(j->arg, j->t, j->lo, j->hi);
-    return NULL;
-}
-
-static uint32_t par_threads(uint32_t n)
-{
-    long c = sysconf(_SC_NPROCESSORS_ONLN);
-    uint32_t t = c > 0 ? (uint32_t)c : 1u;
-    if (t > PAR_MAX) t = PAR_MAX;
-    const uint32_t by_size = n / PAR_MIN_FRAMES;
-    if (t > by_size) t = by_size ? by_size : 1u;
-    return t;
-}
-
-/* runs fn over T ranges (T from par_threads); range 0 on the calling thread.
- * A thread that cannot be created runs its range inline. */
-static void par_for(uint32_t n, uint32_t T, void (*fn)(void *, uint32_t, uint32_t, uint32_t),
-                    void *arg)
-{
-    par_job job[PAR_MAX];
-    pthread_t th[PAR_MAX];
-    int started[PAR_MAX] = {0};
-    for (uint32_t t = 0; t < T; t++) {
-        job[t].fn = fn;
-        job[t].arg = arg;
-        job[t].t = t;
-        job[t].lo = (uint32_t)((uint64_t)n * t / T);
-        job[t].hi = (uint32_t)((uint64_t)n * (t + 1) / T);
-    }
-    for (uint32_t t = 1; t < T; t++)
-        started[t] = pthread_create(&th[t], NULL, par_main, &job[t]) == 0;
-    par_main(&job[0]);
-    for (uint32_t t = 1; t < T; t++) {
-        if (started[t])
-            pthread_join(th[t], NULL);
-        else
-            par_main(&job[t]);
-    }
 }
 
 /* ----------------------------------------------------------------- f1: RX */
@@ -203,90 +146,6 @@ void lvlip_rx_apply(uint32_t n, uint8_t *verdict, uint32_t m, const uint32_t *ta
     }
 }
 
-/* The batch of one call: range t planned its entries into the scratch arrays
- * at 2*lo_t (at most two per frame), then they are packed to off[t]. */
-typedef struct rx_par {
-    const lvlip_frame *frames;
-    uint32_t n, T, flags;
-    uint8_t *verdict;
-    lvlip_csum_iov *iov_s, *iov;
-    uint32_t *tag_s, *tag;
-    const uint16_t *cs;
-    uint32_t m[PAR_MAX], off[PAR_MAX];
-} rx_par;
-
-static void rx_plan_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
-{
-    rx_par *a = (rx_par *)p;
-    a->m[t] = rx_plan_range(a->frames, lo, hi, a->flags, a->verdict, a->iov_s + 2u * (size_t)lo,
-                            a->tag_s + 2u * (size_t)lo);
-}
-
-static void rx_pack_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
-{
-    (void)hi;
-    rx_par *a = (rx_par *)p;
-    memcpy(a->iov + a->off[t], a->iov_s + 2u * (size_t)lo, sizeof(lvlip_csum_iov) * a->m[t]);
-    memcpy(a->tag + a->off[t], a->tag_s + 2u * (size_t)lo, sizeof(uint32_t) * a->m[t]);
-}
-
-static void rx_apply_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
-{
-    (void)lo;
-    (void)hi;
-    rx_par *a = (rx_par *)p;
-    /* a range's entries belong to its own frames only */
-    lvlip_rx_apply(a->n, a->verdict, a->m[t], a->tag + a->off[t], a->cs + a->off[t]);
-}
-
-/* Round 4's host frame path (hidden; frames_host.cpp runs it under
- * LVLIP_FRAME_PATH=hostplan): plan every frame on the CPU, one
- * lvlip_csum_batch_host over the planned pieces, apply. */
-int lvlip_rx_verify_hostplan(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n,
-                             uint32_t flags, uint8_t *verdict);
-int lvlip_tx_checksum_hostplan(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n);
-
-int lvlip_rx_verify_hostplan(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n,
-                             uint32_t flags, uint8_t *verdict)
-{
-    /* two checksums per frame at most: 2n must fit one batch (as the _dev call) */
-    if (!ctx || (n && (!frames || !verdict)) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
-    if (n == 0) return LVLIP_OK;
-    rx_par a;
-    memset(&a, 0, sizeof a);
-    a.frames = frames;
-    a.n = n;
-    a.T = par_threads(n);
-    a.flags = flags;
-    a.verdict = verdict;
-    a.iov_s = (lvlip_csum_iov *)malloc(sizeof(lvlip_csum_iov) * 2u * (size_t)n);
-    a.iov = (lvlip_csum_iov *)malloc(sizeof(lvlip_csum_iov) * 2u * (size_t)n);
-    a.tag_s = (uint32_t *)malloc(sizeof(uint32_t) * 2u * (size_t)n);
-    a.tag = (uint32_t *)malloc(sizeof(uint32_t) * 2u * (size_t)n);
-    uint16_t *cs = (uint16_t *)malloc(sizeof(uint16_t) * 2u * (size_t)n);
-    int rc = LVLIP_ENOMEM;
-    if (a.iov_s && a.iov && a.tag_s && a.tag && cs) {
-        par_for(n, a.T, rx_plan_job, &a);
-        uint32_t m = 0;
-        for (uint32_t t = 0; t < a.T; t++) {
-            a.off[t] = m;
-            m += a.m[t];
-        }
-        par_for(n, a.T, rx_pack_job, &a);
-        rc = m ? lvlip_csum_batch_host(ctx, a.iov, m, cs) : LVLIP_OK;
-        if (rc == LVLIP_OK) {
-            a.cs = cs;
-            par_for(n, a.T, rx_apply_job, &a);
-        }
-    }
-    free(a.iov_s);
-    free(a.iov);
-    free(a.tag_s);
-    free(a.tag);
-    free(cs);
-    return rc;
-}
-
 /* ----------------------------------------------------------------- f2: TX */
 
 static uint32_t tx_plan_range(lvlip_frame *frames, uint32_t lo, uint32_t hi, lvlip_csum_iov *iov,
@@ -337,97 +196,6 @@ uint32_t lvlip_tx_plan(lvlip_frame *frames, uint32_t n, lvlip_csum_iov *iov, uin
 void lvlip_tx_apply(uint32_t m, uint8_t *const *field, const uint16_t *csum)
 {
     for (uint32_t k = 0; k < m; k++) memcpy(field[k], &csum[k], 2); /* raw store */
-}
-
-static int tx_frame_ok(const lvlip_frame *f)
-{
-    const uint8_t *h = f->head;
-    if (!h || f->len < ETH_HDR_LEN + 20u) return 0;
-    const uint8_t *ih = h + ETH_HDR_LEN;
-    const uint32_t ihl = ih[0] & 0x0fu, iplen = be16(ih + 2);
-    return (ih[0] >> 4) == 4u && ihl >= 5u && iplen >= ihl * 4u && f->len >= ETH_HDR_LEN + iplen;
-}
-
-typedef struct tx_par {
-    lvlip_frame *frames;
-    uint32_t n, T;
-    lvlip_csum_iov *iov_s, *iov;
-    uint8_t **field_s, **field;
-    const uint16_t *cs;
-    uint32_t bad[PAR_MAX], m[PAR_MAX], off[PAR_MAX];
-} tx_par;
-
-static void tx_check_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
-{
-    tx_par *a = (tx_par *)p;
-    a->bad[t] = 0;
-    for (uint32_t i = lo; i < hi && !a->bad[t]; i++) {
-        pf_header(a->frames, i, hi);
-        a->bad[t] = !tx_frame_ok(&a->frames[i]);
-    }
-}
-
-static void tx_plan_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
-{
-    tx_par *a = (tx_par *)p;
-    a->m[t] = tx_plan_range(a->frames, lo, hi, a->iov_s + 2u * (size_t)lo, a->field_s + 2u * (size_t)lo);
-}
-
-static void tx_pack_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
-{
-    (void)hi;
-    tx_par *a = (tx_par *)p;
-    memcpy(a->iov + a->off[t], a->iov_s + 2u * (size_t)lo, sizeof(lvlip_csum_iov) * a->m[t]);
-    memcpy(a->field + a->off[t], a->field_s + 2u * (size_t)lo, sizeof(uint8_t *) * a->m[t]);
-}
-
-static void tx_apply_job(void *p, uint32_t t, uint32_t lo, uint32_t hi)
-{
-    (void)lo;
-    (void)hi;
-    tx_par *a = (tx_par *)p;
-    lvlip_tx_apply(a->m[t], a->field + a->off[t], a->cs + a->off[t]);
-}
-
-int lvlip_tx_checksum_hostplan(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n)
-{
-    if (!ctx || (n && !frames) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
-    if (n == 0) return LVLIP_OK;
-    tx_par a;
-    memset(&a, 0, sizeof a);
-    a.frames = frames;
-    a.n = n;
-    a.T = par_threads(n);
-    /* validate every frame before touching any of them */
-    par_for(n, a.T, tx_check_job, &a);
-    for (uint32_t t = 0; t < a.T; t++)
-        if (a.bad[t]) return LVLIP_EINVAL;
-    a.iov_s = (lvlip_csum_iov *)malloc(sizeof(lvlip_csum_iov) * 2u * (size_t)n);
-    a.iov = (lvlip_csum_iov *)malloc(sizeof(lvlip_csum_iov) * 2u * (size_t)n);
-    a.field_s = (uint8_t **)malloc(sizeof(uint8_t *) * 2u * (size_t)n);
-    a.field = (uint8_t **)malloc(sizeof(uint8_t *) * 2u * (size_t)n);
-    uint16_t *cs = (uint16_t *)malloc(sizeof(uint16_t) * 2u * (size_t)n);
-    int rc = LVLIP_ENOMEM;
-    if (a.iov_s && a.iov && a.field_s && a.field && cs) {
-        par_for(n, a.T, tx_plan_job, &a);
-        uint32_t m = 0;
-        for (uint32_t t = 0; t < a.T; t++) {
-            a.off[t] = m;
-            m += a.m[t];
-        }
-        par_for(n, a.T, tx_pack_job, &a);
-        rc = lvlip_csum_batch_host(ctx, a.iov, m, cs);
-        if (rc == LVLIP_OK) {
-            a.cs = cs;
-            par_for(n, a.T, tx_apply_job, &a);
-        }
-    }
-    free(a.iov_s);
-    free(a.iov);
-    free(a.field_s);
-    free(a.field);
-    free(cs);
-    return rc;
 }
 
 /* ----------------------------------------------------------------- f4: RFC 1624 */

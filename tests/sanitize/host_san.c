@@ -5,23 +5,23 @@
  * level-ip's `make debug` builds with -fsanitize=thread
  * (Makefile:17-18) and its test runner greps ThreadSanitizer reports
  * (tests/test-run-all:41).  The counterpart here builds the per-call drop-in
- * (level-ip_amd/csrc/csum_cpu.c) and the frame calls' host steps
- * (level-ip_amd/csrc/skb_batch.c: plan / pack / apply over up to 16 threads)
- * with ASan + UBSan, and again with TSan, and drives them with:
+ * (level-ip_amd/csrc/csum_cpu.c) and the exported frame plan / apply steps
+ * (level-ip_amd/csrc/skb_batch.c) with ASan + UBSan, and again with TSan, and
+ * drives them with:
  *   1. every length 0..600 plus MTU/jumbo/64 KiB sizes at all 16 alignments,
  *      each buffer allocated to its exact end, checked against the oracle;
  *   2. eight threads calling checksum / tcp_udp_checksum at once (the
  *      reference calls checksum() from its core, IPC and timer threads);
  *   3. 40 000 frames, each in an allocation of exactly its length, through
- *      the host-plan frame path (skb_batch.c's lvlip_tx_checksum_hostplan and
- *      lvlip_rx_verify_hostplan, several host threads; the product's
- *      lvlip_tx_checksum / lvlip_rx_verify run it under
- *      LVLIP_FRAME_PATH=hostplan), plus malformed frames that must be refused
- *      without reading past their ends.
+ *      lvlip_tx_plan / lvlip_tx_apply and lvlip_rx_plan / lvlip_rx_apply with
+ *      the oracle summing the planned entries, plus malformed frames that must
+ *      be refused (TX) or given their verdict (RX) without reading past their
+ *      ends.
  *
- * The GPU batch between the host steps (lvlip_csum_batch_host, csum_ctx.cpp)
- * is replaced below by the oracle: the host code around it is what is under
- * test; tests/test_skb_gpu.py runs the same calls with the real batch.
+ * The product's host frame calls (frames_host.cpp, HIP host code) run under
+ * ASan/TSan in tests/sanitize/frames_san.cpp; the skb-queue walkers of
+ * skb_batch.c, which call them, are linked here against the plan + oracle
+ * compositions below.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -37,11 +37,6 @@ uint16_t oracle_checksum(const void *addr, int count, int start_sum);
 int oracle_tcp_udp_checksum(uint32_t saddr, uint32_t daddr, uint8_t proto, const uint8_t *data,
                             uint16_t len);
 
-/* skb_batch.c (hidden in the library) */
-int lvlip_rx_verify_hostplan(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n,
-                             uint32_t flags, uint8_t *verdict);
-int lvlip_tx_checksum_hostplan(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n);
-
 static int g_fail;
 #define CHECK(c, ...)                                            \
     do {                                                         \
@@ -53,26 +48,50 @@ static int g_fail;
         }                                                        \
     } while (0)
 
-/* stand-in for the GPU batch (see the header comment) */
-int lvlip_csum_batch_host(lvlip_csum_ctx *ctx, const lvlip_csum_iov *p, uint32_t n,
-                          uint16_t *out)
+/* The frame calls' decisions as the exported host steps (plan, the oracle
+ * over the planned entries, apply): stand-ins for the product's calls
+ * (frames_host.cpp), which skb_batch.c's skb-queue walkers reach. */
+static void sum_entries(const lvlip_csum_iov *iov, uint32_t m, uint16_t *cs)
 {
-    (void)ctx;
-    for (uint32_t i = 0; i < n; i++)
-        out[i] = oracle_checksum(p[i].ptr, p[i].len, (int)p[i].start_sum);
-    return LVLIP_OK;
+    for (uint32_t k = 0; k < m; k++) cs[k] = oracle_checksum(iov[k].ptr, iov[k].len, (int)iov[k].start_sum);
 }
 
-/* stand-ins for the product's frame calls (frames_host.cpp, HIP host code),
- * which skb_batch.c's skb-queue walkers call: the host-plan path here */
 int lvlip_rx_verify(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n, uint32_t flags,
                     uint8_t *verdict)
 {
-    return lvlip_rx_verify_hostplan(ctx, frames, n, flags, verdict);
+    if (!ctx || (n && (!frames || !verdict))) return LVLIP_EINVAL;
+    if (n == 0) return LVLIP_OK;
+    lvlip_csum_iov *iov = malloc(sizeof *iov * 2u * n);
+    uint32_t *tag = malloc(sizeof *tag * 2u * n);
+    uint16_t *cs = malloc(sizeof *cs * 2u * n);
+    const uint32_t m = lvlip_rx_plan(frames, n, flags, verdict, iov, tag);
+    sum_entries(iov, m, cs);
+    lvlip_rx_apply(n, verdict, m, tag, cs);
+    free(iov);
+    free(tag);
+    free(cs);
+    return LVLIP_OK;
 }
+
 int lvlip_tx_checksum(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n)
 {
-    return lvlip_tx_checksum_hostplan(ctx, frames, n);
+    if (!ctx || (n && !frames)) return LVLIP_EINVAL;
+    if (n == 0) return LVLIP_OK;
+    lvlip_csum_iov *iov = malloc(sizeof *iov * 2u * n);
+    uint8_t **field = malloc(sizeof *field * 2u * n);
+    uint16_t *cs = malloc(sizeof *cs * 2u * n);
+    /* the plan reads and refuses before anything is written */
+    const uint32_t m = lvlip_tx_plan(frames, n, iov, field);
+    int rc = LVLIP_EINVAL;
+    if (m != 0xFFFFFFFFu) {
+        sum_entries(iov, m, cs);
+        lvlip_tx_apply(m, field, cs);
+        rc = LVLIP_OK;
+    }
+    free(iov);
+    free(field);
+    free(cs);
+    return rc;
 }
 
 static uint64_t g_rng = 0x1E7E1C5ull;
@@ -187,7 +206,7 @@ static void frames(void)
     for (uint32_t i = 0; i < n; i++) fr[i] = make_frame((rnd() & 1u) != 0);
     lvlip_csum_ctx *ctx = (lvlip_csum_ctx *)(void *)&g_fail; /* opaque, unused by the stand-in */
 
-    CHECK(lvlip_tx_checksum_hostplan(ctx, fr, n) == LVLIP_OK, "tx");
+    CHECK(lvlip_tx_checksum(ctx, fr, n) == LVLIP_OK, "tx");
     for (uint32_t i = 0; i < n; i++) {
         uint8_t *ih = fr[i].head + 14;
         const uint32_t ihl = ih[0] & 15u, iplen = ((uint32_t)ih[2] << 8) | ih[3];
@@ -211,13 +230,13 @@ static void frames(void)
     uint8_t *v = (uint8_t *)malloc(n);
     for (uint32_t flags = 0; flags <= LVLIP_RX_VERIFY_L4; flags++) {
         memset(v, 0, n);
-        CHECK(lvlip_rx_verify_hostplan(ctx, fr, n, flags, v) == LVLIP_OK, "rx");
+        CHECK(lvlip_rx_verify(ctx, fr, n, flags, v) == LVLIP_OK, "rx");
         uint32_t ok = 0;
         for (uint32_t i = 0; i < n; i++) ok += v[i] == LVLIP_RX_OK;
         CHECK(ok == n, "rx flags %u: %u of %u ok", flags, ok, n);
     }
 
-    /* malformed frames: each kind in the middle of a multi-threaded batch, in
+    /* malformed frames: each kind in the middle of a batch, in
      * an allocation that ends where the frame's len says */
     for (uint32_t k = 0; k < 8; k++) {
         const uint32_t at = n / 2u + k;
@@ -243,11 +262,11 @@ static void frames(void)
         if (k != 6 && k != 7) { /* 6 and 7 are well-formed IPv4 as far as TX cares */
             uint8_t *snap = (uint8_t *)malloc(bad.len);
             memcpy(snap, bad.head, bad.len);
-            CHECK(lvlip_tx_checksum_hostplan(ctx, fr, n) == LVLIP_EINVAL, "tx kind %u refused", k);
+            CHECK(lvlip_tx_checksum(ctx, fr, n) == LVLIP_EINVAL, "tx kind %u refused", k);
             CHECK(memcmp(snap, bad.head, bad.len) == 0, "tx kind %u untouched", k);
             free(snap);
         }
-        CHECK(lvlip_rx_verify_hostplan(ctx, fr, n, LVLIP_RX_VERIFY_L4, v) == LVLIP_OK, "rx kind %u", k);
+        CHECK(lvlip_rx_verify(ctx, fr, n, LVLIP_RX_VERIFY_L4, v) == LVLIP_OK, "rx kind %u", k);
         if (want_rx != 0xff)
             CHECK(v[at] == want_rx, "rx kind %u: verdict %u want %u", k, v[at], want_rx);
         else
@@ -256,9 +275,9 @@ static void frames(void)
         free(bad.head);
         fr[at] = keep;
     }
-    CHECK(lvlip_rx_verify_hostplan(ctx, fr, 0, 0, v) == LVLIP_OK && lvlip_tx_checksum_hostplan(ctx, fr, 0) == LVLIP_OK,
+    CHECK(lvlip_rx_verify(ctx, fr, 0, 0, v) == LVLIP_OK && lvlip_tx_checksum(ctx, fr, 0) == LVLIP_OK,
           "n = 0");
-    CHECK(lvlip_rx_verify_hostplan(NULL, fr, n, 0, v) == LVLIP_EINVAL, "NULL ctx");
+    CHECK(lvlip_rx_verify(NULL, fr, n, 0, v) == LVLIP_EINVAL, "NULL ctx");
     for (uint32_t i = 0; i < n; i++) free(fr[i].head);
     free(fr);
     free(v);

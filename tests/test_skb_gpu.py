@@ -244,23 +244,6 @@ def test_rx_verify_skb_buffers_longer_than_frames(ctx):
     assert (got == lvlip.RX_OK).sum() > 3500
 
 
-def test_host_frames_hostplan_ab_agrees(monkeypatch):
-    """LVLIP_FRAME_PATH=hostplan (round 4's host path, kept for A/B) and the
-    product's device-parse path give the same fill and verdicts."""
-    fr = workloads.frames(8000, seed=92, max_l4=1460)
-    a, b = [bytearray(f) for f in fr], [bytearray(f) for f in fr]
-    monkeypatch.setenv("LVLIP_FRAME_PATH", "hostplan")
-    with lvlip.Context(0, arena_bytes=4 << 20) as hp:
-        hp.tx_checksum(a)
-        va = [hp.rx_verify(a, fl) for fl in (0, lvlip.RX_VERIFY_L4)]
-    monkeypatch.delenv("LVLIP_FRAME_PATH")
-    with lvlip.Context(0, arena_bytes=4 << 20) as dp:
-        dp.tx_checksum(b)
-        vb = [dp.rx_verify(b, fl) for fl in (0, lvlip.RX_VERIFY_L4)]
-    assert [bytes(x) for x in a] == [bytes(x) for x in b]
-    assert all(np.array_equal(x, y) for x, y in zip(va, vb))
-
-
 # ------------------------------------------------- device-resident frames --
 
 def _dev(buf):
