@@ -294,9 +294,13 @@ int frames_zerocopy(lvlip_csum_ctx* c, const Region& r, const lvlip_frame* fr, u
 }
 
 // Frames inside one LVLIP_REG_DMA region: a piece is a run of frames whose
-// byte span [lo, hi) (lo rounded down to 16, so every frame keeps its address
-// mod 16) fits the piece size; the copy engine reads the span from the region.
-int frames_dma(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out, PieceDone* cb) {
+// byte span [lo, hi) fits the piece size; the copy engine reads the span from
+// the region.  lo is rounded down to 16 from the region's first byte, not from
+// address 0, so the span never starts before the registered bytes (the copy
+// engine reads them as pinned memory; the kernels take any alignment).
+int frames_dma(lvlip_csum_ctx* c, const Region& r, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out,
+               PieceDone* cb) {
+    const uintptr_t r0 = (uintptr_t)r.host;
     const uint32_t fmax = frames_per_piece(c, mode), ob = out_bytes(mode);
     FrameSlots fs{c, cb};
     int cur = 0;
@@ -311,9 +315,10 @@ int frames_dma(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, u
         const uint64_t pb = piece_bytes(c, idx++);
         while (i < n && k < fmax) {
             const uintptr_t a = (uintptr_t)fr[i].head, e = a + fr[i].len;
-            const uintptr_t nlo = (a & ~(uintptr_t)15) < lo ? (a & ~(uintptr_t)15) : lo;
+            const uintptr_t a16 = r0 + ((a - r0) & ~(uintptr_t)15);
+            const uintptr_t nlo = a16 < lo ? a16 : lo;
             const uintptr_t nhi = e > hi ? e : hi;
-            if (align16(nhi) - nlo > (k ? pb : c->arena)) break;  // k = 0: fits (checked)
+            if (align16(nhi - nlo) > (k ? pb : c->arena)) break;  // k = 0: fits (checked)
             lo = nlo;
             hi = nhi;
             ++k;
@@ -368,7 +373,7 @@ int frames_run_(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, 
                 sum += fr[i].len;
                 fits = fits && align16(fr[i].len + 15u) <= c->arena;
             }
-            if (fits && hi - lo <= 2 * sum + (1ull << 20)) return frames_dma(c, fr, n, mode, out, cb);
+            if (fits && hi - lo <= 2 * sum + (1ull << 20)) return frames_dma(c, *r, fr, n, mode, out, cb);
         }
     }
     // scattered: every frame's slot offset (a prefix sum over the frames'

@@ -8,7 +8,9 @@
 // the copies (LVLIP_DIRECT_MAX=0); frames come scattered, in a slab registered
 // for DMA and for zero-copy (shuffled order), as BUFLEN-long RX skbs, with a
 // malformed frame in a late piece (every frame must come back untouched), and
-// from three contexts on three threads at once.
+// from three contexts on three threads at once.  One more slab per kind is
+// registered from an address that is not 16-B aligned, with the bytes before
+// it poisoned under ASan: no copy may start before a region's first byte.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -20,6 +22,16 @@
 
 #include "lvlip_csum.h"
 #include "lvlip_skb.h"
+
+#if defined(__SANITIZE_ADDRESS__)  // gcc's -fsanitize=address (the test builds with g++)
+#include <sanitizer/asan_interface.h>
+#define POISON(p, n) __asan_poison_memory_region((p), (n))
+#define UNPOISON(p, n) __asan_unpoison_memory_region((p), (n))
+#endif
+#ifndef POISON
+#define POISON(p, n) ((void)(p), (void)(n))
+#define UNPOISON(p, n) ((void)(p), (void)(n))
+#endif
 
 extern "C" uint16_t oracle_checksum(const void* addr, int count, int start_sum);
 extern "C" int oracle_tcp_udp_checksum(uint32_t saddr, uint32_t daddr, uint8_t proto, const uint8_t* data,
@@ -128,7 +140,11 @@ static void scattered(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed) {
     for (auto& f : fr) free(f.head);
 }
 
-static void slab(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed, uint32_t reg) {
+// lead > 0: the region starts lead bytes into its allocation (not 16-B
+// aligned), the first frame at its first byte, the lead bytes poisoned (ASan
+// poisons whole 8-B granules from the allocation's start: lead 13 poisons
+// the first 8, which a span rounded down to 16 from address 0 would read).
+static void slab(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed, uint32_t reg, uint32_t lead = 0) {
     Rng r{seed};
     std::vector<uint32_t> len(n), off(n), ihl(n), l4h(n);
     std::vector<bool> tcp(n);
@@ -137,11 +153,13 @@ static void slab(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed, uint32_t reg) {
         bool t;
         len[i] = frame_len(r, t, ihl[i], l4h[i]);
         tcp[i] = t;
-        pos += r() % 24u;
+        if (i || !lead) pos += r() % 24u;
         off[i] = (uint32_t)pos;
         pos += len[i];
     }
-    uint8_t* s = (uint8_t*)malloc(pos);
+    uint8_t* raw = (uint8_t*)malloc(lead + pos);
+    uint8_t* s = raw + lead;
+    POISON(raw, lead);
     for (uint32_t i = 0; i < n; ++i) fill_frame(r, s + off[i], len[i], tcp[i], ihl[i], l4h[i]);
     CHECK(lvlip_csum_register(ctx, s, pos, reg) == LVLIP_OK, "register");
     std::vector<lvlip_frame> fr(n);
@@ -176,7 +194,8 @@ static void slab(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed, uint32_t reg) {
     CHECK(lvlip_rx_verify(ctx, sk.data(), m, LVLIP_RX_VERIFY_L4, v.data()) == LVLIP_OK, "rx skbs");
     for (uint32_t i = 0; i < m; ++i) CHECK(v[i] == want[i], "rx skb %u: %u want %u", i, v[i], want[i]);
     for (auto* b : bufs) free(b);
-    free(s);
+    UNPOISON(raw, lead);
+    free(raw);
 }
 
 // The packet batches of the same context (csum_ctx.cpp): scattered exact-size
@@ -224,6 +243,8 @@ int main() {
         packets(ctx, 12000, 7 + direct);
         slab(ctx, 12000, 3 + direct, LVLIP_REG_DMA);
         slab(ctx, 6000, 5 + direct, LVLIP_REG_ZEROCOPY);
+        slab(ctx, 4000, 9 + direct, LVLIP_REG_DMA, 13);
+        slab(ctx, 4000, 13 + direct, LVLIP_REG_ZEROCOPY, 13);
         CHECK(lvlip_csum_ctx_destroy(ctx) == LVLIP_OK, "destroy");
     }
     unsetenv("LVLIP_DIRECT_MAX");
