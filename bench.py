@@ -772,6 +772,18 @@ def cpu_header_check(lvlip, host, fd, budget_s=0.3):
                 pyoracle.batch(host, dd, threads=1, **kw)
                 reps += 1
             res[name.replace("_ns", tag + "_ns")] = round((time.perf_counter() - t0) / reps / dd.size * 1e9, 2)
+    # what the RX + L4 call does per frame, on one core with the drop-in: the
+    # 20-B header and the TCP/ICMP segment after it (two checksums per frame)
+    d2 = np.zeros(2 * fd.size, dtype=lvlip.DESC_DTYPE)
+    d2["offset"][0::2] = fd["offset"] + 14
+    d2["len"][0::2] = 20
+    d2["offset"][1::2] = fd["offset"] + 34
+    d2["len"][1::2] = np.maximum(fd["len"].astype(np.int64) - 34, 0)
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        pyoracle.batch(host, d2, threads=1, csum_fn=lvlip.lib().checksum)
+        reps += 1
+    res["dropin_header_l4_ns_per_frame"] = round((time.perf_counter() - t0) / reps / fd.size * 1e9, 2)
     return res
 
 
@@ -789,8 +801,13 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
       zerocopy   the slab registered LVLIP_REG_ZEROCOPY (kernel reads in place)
       scattered_t8  scattered with 8 gather threads (LVLIP_GATHER_THREADS;
                  the default is min(hardware threads, 16), round 4's was 8)
+      slab_spin, dma_spin  slab and dma with every piece waited for by
+                 spinning (LVLIP_BLOCK_MIN=0; the default sleeps on pieces
+                 from 4 MiB)
     GB/s counts the checksummed bytes (20 B header + L4 per frame) as the
-    device lines do; frame_GBps counts the frames' bytes (what crosses PCIe)."""
+    device lines do; frame_GBps counts the frames' bytes (what crosses PCIe);
+    cpu_ns_per_frame is the process's CPU time (all threads) per frame, what
+    the call costs the host beside the CPU's own checksum (cpu_header_check)."""
     import ctypes
 
     n = fd.size
@@ -825,13 +842,17 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
             assert call() == 0, (tag, name)
             if name == "rx_header":  # filled by tx_fill (L4: the lossy TCP seed may not verify)
                 assert (verdict == lvlip.RX_OK).all(), (tag, name)
-            t0 = time.perf_counter()
+            t0, c0 = time.perf_counter(), time.process_time()
             for _ in range(5):
                 assert call() == 0, (tag, name)
             ms = (time.perf_counter() - t0) / 5 * 1e3
+            cpu_ms = (time.process_time() - c0) / 5 * 1e3
             nb = 20 * n if name == "rx_header" else hb
             r[name] = {"ms": round(ms, 3), "Mframes_per_s": round(n / ms / 1e3, 2),
-                       "GBps": round(nb / ms / 1e6, 2)}
+                       "GBps": round(nb / ms / 1e6, 2),
+                       # CPU time of the whole process (every thread: the
+                       # caller's wait, the pool's gather and apply) per frame
+                       "cpu_ns_per_frame": round(cpu_ms * 1e6 / n, 2)}
             if name != "rx_header":
                 r[name]["frame_GBps"] = round(frame_bytes / ms / 1e6, 2)
         out[tag] = r
@@ -849,12 +870,20 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
                 run(ctx, keep_slab[1], tag)
             finally:
                 ctx.unregister(host)
-    for env, tag, arr in (("LVLIP_GATHER_THREADS=8", "scattered_t8", keep_scat[1]),):
+    for env, tag, arr, flag in (("LVLIP_GATHER_THREADS=8", "scattered_t8", keep_scat[1], None),
+                                ("LVLIP_BLOCK_MIN=0", "slab_spin", keep_slab[1], None),
+                                ("LVLIP_BLOCK_MIN=0", "dma_spin", keep_slab[1], lvlip.REG_DMA)):
         k, v = env.split("=")
         os.environ[k] = v
         try:
             with lvlip.Context(d) as ctx:
-                run(ctx, arr, tag)
+                if flag is not None:
+                    ctx.register(host, flag)
+                try:
+                    run(ctx, arr, tag)
+                finally:
+                    if flag is not None:
+                        ctx.unregister(host)
         finally:
             del os.environ[k]
     out["cpu_header_check"] = cpu_header_check(lvlip, host, fd)

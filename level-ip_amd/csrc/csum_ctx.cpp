@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <string>
 #include <thread>
@@ -26,6 +27,7 @@ namespace {
 constexpr size_t kDefaultArena = 64ull << 20;
 constexpr uint64_t kDirectMax = 4ull << 20;  // measured: DESIGN.md §5
 constexpr uint64_t kPieceMax = 32ull << 20;  // measured: DESIGN.md §5
+constexpr uint64_t kBlockMin = 4ull << 20;   // ~80 us of PCIe: DESIGN.md §9
 
 }  // namespace
 
@@ -42,16 +44,24 @@ int fail(lvlip_csum_ctx* c, hipError_t e, const char* what, int code) {
 
 int drain(lvlip_csum_ctx* c, Slot& s) {
     if (!s.busy) return LVLIP_OK;
-    hipError_t e = hipEventSynchronize(s.done);
+    hipError_t e = hipSuccess;
+    if (s.sleep) {
+        // hipEventSynchronize spins (with or without hipEventBlockingSync, as
+        // measured: DESIGN.md §9), so a long piece is polled between 20-us sleeps
+        const timespec nap{0, 20000};
+        while ((e = hipEventQuery(s.done)) == hipErrorNotReady) nanosleep(&nap, nullptr);
+    }
+    if (e == hipSuccess) e = hipEventSynchronize(s.done);
     s.busy = false;
     if (e != hipSuccess) return fail(c, e, "hipEventSynchronize");
     memcpy(s.user_out, s.h_out, s.out_bytes);
     return LVLIP_OK;
 }
 
-int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes) {
+int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes, uint64_t piece_bytes) {
     const hipError_t e = hipEventRecord(s.done, s.stream);
     if (e != hipSuccess) return fail(c, e, "hipEventRecord");
+    s.sleep = c->block_min && piece_bytes >= c->block_min;
     s.user_out = user_out;
     s.out_bytes = out_bytes;
     s.busy = true;
@@ -111,7 +121,7 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
         const int rc = lvlip_csum_batch_dev_ex(dev_base ? dev_base : s.dh_bytes, s.dh_desc, count,
                                                s.dh_out, s.stream, &cfg);
         if (rc != LVLIP_OK) return rc;
-        return arm_slot(c, s, user_out, (size_t)count * sizeof(uint16_t));
+        return arm_slot(c, s, user_out, (size_t)count * sizeof(uint16_t), bytes);
     }
     if (!dev_base) {
         const uint64_t nb = src && src != s.h_bytes ? bytes : align16(bytes);
@@ -128,7 +138,7 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
     if ((e = hipMemcpyAsync(s.h_out, s.d_out, (size_t)count * sizeof(uint16_t),
                             hipMemcpyDeviceToHost, s.stream)) != hipSuccess)
         return fail(c, e, "D2H results");
-    return arm_slot(c, s, user_out, (size_t)count * sizeof(uint16_t));
+    return arm_slot(c, s, user_out, (size_t)count * sizeof(uint16_t), bytes);
 }
 
 // Zero-copy: descriptors only (offsets from the region's first byte rounded
@@ -207,6 +217,15 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         const char* e = getenv("LVLIP_FIRST_PIECE");
         const long long v = e ? atoll(e) : 0;
         c->first_piece = v > 0 ? align16((uint64_t)v) : (4ull << 20);
+    }
+    // LVLIP_BLOCK_MIN: a piece of at least this many bytes is waited for by
+    // polling between short sleeps instead of by spinning: the pipeline's
+    // other slot keeps the GPU busy meanwhile, so the late wake-up costs no
+    // throughput and the waiting thread little CPU (0: always spin)
+    {
+        const char* e = getenv("LVLIP_BLOCK_MIN");
+        const long long v = e ? atoll(e) : (long long)kBlockMin;
+        c->block_min = v > 0 ? (uint64_t)v : 0u;
     }
     {
         const char* e = getenv("LVLIP_FRAME_TRACE");

@@ -44,6 +44,11 @@ struct Slot {
     uint16_t* d_out = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    // how drain() waits for `done`: spinning in hipEventSynchronize (short
+    // pieces: the lowest latency), or polling it between short sleeps (long
+    // pieces: the waiting thread costs no CPU while the other slot's piece
+    // keeps the GPU busy)
+    bool sleep = false;
     // piece bookkeeping: the in-flight piece's results (out_bytes of them in
     // h_out) go to user_out when the slot drains
     void* user_out = nullptr;
@@ -70,6 +75,7 @@ struct lvlip_csum_ctx {
     uint64_t direct_max = 0;  // pieces up to this many bytes skip the copies
     uint64_t piece = 0;       // bytes per piece (<= arena; a larger packet gets its own)
     uint64_t first_piece = 0; // frame calls: the first piece's bytes (doubling up to `piece`)
+    uint64_t block_min = 0;   // pieces of at least this many bytes are waited for asleep (0: never)
     // frame calls' per-call host arrays (TX records and undo values, RX + L4
     // lengths), kept across calls: fresh pages would fault on every call
     void* frame_scratch = nullptr;
@@ -95,7 +101,9 @@ int finish_pieces(lvlip_csum_ctx* c, int rc);
 // The registered region holding [p, p + len), or nullptr.
 const Region* find_region(const lvlip_csum_ctx* c, const void* p, uint64_t len);
 // Marks the slot busy with a piece whose results (out_bytes) go to user_out.
-int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes);
+// records the slot's completion after its piece of `piece_bytes` bytes; the
+// wait for it sleeps from c->block_min bytes up, else spins
+int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes, uint64_t piece_bytes);
 
 struct DeviceGuard {
     int prev = -1;

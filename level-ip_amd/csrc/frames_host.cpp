@@ -171,7 +171,7 @@ int launch_frame_piece(lvlip_csum_ctx* c, Slot& s, int mode, uint64_t bytes, uin
         const int rc = lvlip_frames_host_launch(mode, dev_base ? dev_base : s.dh_bytes,
                                                 (const lvlip_frame_desc*)s.dh_desc, k, s.dh_out, s.stream);
         if (rc != LVLIP_OK) return rc;
-        return arm_slot(c, s, user_out, nout);
+        return arm_slot(c, s, user_out, nout, bytes);
     }
     if (!dev_base) {
         const uint64_t nb = src ? bytes : align16(bytes);
@@ -187,7 +187,7 @@ int launch_frame_piece(lvlip_csum_ctx* c, Slot& s, int mode, uint64_t bytes, uin
     if (rc != LVLIP_OK) return rc;
     if ((e = hipMemcpyAsync(s.h_out, s.d_out, nout, hipMemcpyDeviceToHost, s.stream)) != hipSuccess)
         return fail(c, e, "D2H frame results");
-    return arm_slot(c, s, user_out, nout);
+    return arm_slot(c, s, user_out, nout, bytes);
 }
 
 // Scattered frames: each frame's need_len bytes (len[i] when given) copied
@@ -333,20 +333,55 @@ int frames_dma(lvlip_csum_ctx* c, const Region& r, const lvlip_frame* fr, uint32
     return fs.finish(rc, cur);
 }
 
-// The region holding every frame, or nullptr.
-const Region* one_region(const lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n) {
-    if (c->regions.empty()) return nullptr;
+// The region holding every frame (nullptr if there is none), with what the
+// DMA decision needs of the frames: their byte span [lo, hi), their total
+// length, and whether each one's 16-B span fits the arena.  One pass over the
+// frame array on the pool threads (it precedes the first piece).
+struct RegionScan {
     const Region* r = nullptr;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (!fr[i].head) return nullptr;
-        const Region* ri = (r && (const uint8_t*)fr[i].head >= r->host &&
-                            (const uint8_t*)fr[i].head + fr[i].len <= r->host + r->bytes)
-                               ? r
-                               : find_region(c, fr[i].head, fr[i].len);
-        if (!ri || (r && ri != r)) return nullptr;
-        r = ri;
+    uintptr_t lo = ~(uintptr_t)0, hi = 0;
+    uint64_t sum = 0;
+    bool fits = true;
+};
+RegionScan scan_region(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n) {
+    RegionScan out;
+    if (c->regions.empty() || !fr[0].head) return out;
+    const Region* r = find_region(c, fr[0].head, fr[0].len);
+    if (!r) return out;
+    constexpr uint32_t kParts = 256;
+    struct Part {
+        uintptr_t lo, hi;
+        uint64_t sum;
+        bool in, fits;
+    } part[kParts];
+    const uint32_t np = n < kParts ? n : kParts;
+    const uint8_t *r0 = r->host, *r1 = r->host + r->bytes;
+    const uint64_t arena = c->arena;
+    parallel_ranges(c, np, 1, [&](uint64_t plo, uint64_t phi) {
+        for (uint64_t j = plo; j < phi; ++j) {
+            Part p{~(uintptr_t)0, 0, 0, true, true};
+            const uint32_t a = (uint32_t)((uint64_t)n * j / np), b = (uint32_t)((uint64_t)n * (j + 1) / np);
+            for (uint32_t i = a; i < b; ++i) {
+                const uint8_t* h = (const uint8_t*)fr[i].head;
+                p.in = p.in && h && h >= r0 && h + fr[i].len <= r1;
+                const uintptr_t x = (uintptr_t)h, e = x + fr[i].len;
+                p.lo = x < p.lo ? x : p.lo;
+                p.hi = e > p.hi ? e : p.hi;
+                p.sum += fr[i].len;
+                p.fits = p.fits && align16((uint64_t)fr[i].len + 15u) <= arena;
+            }
+            part[j] = p;
+        }
+    });
+    for (uint32_t j = 0; j < np; ++j) {
+        if (!part[j].in) return RegionScan{};
+        out.lo = part[j].lo < out.lo ? part[j].lo : out.lo;
+        out.hi = part[j].hi > out.hi ? part[j].hi : out.hi;
+        out.sum += part[j].sum;
+        out.fits = out.fits && part[j].fits;
     }
-    return r;
+    out.r = r;
+    return out;
 }
 
 // Runs the device step over all n frames; out gets n results (records or
@@ -354,7 +389,8 @@ const Region* one_region(const lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_
 int frames_run_(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out,
                 PieceDone* cb) {
     DeviceGuard g(c->device);
-    if (const Region* r = one_region(c, fr, n)) {
+    const RegionScan rs = scan_region(c, fr, n);
+    if (const Region* r = rs.r) {
         if (r->flags & LVLIP_REG_ZEROCOPY) return frames_zerocopy(c, *r, fr, n, mode, out, cb);
         // a DMA region: the spans, except for the header-only RX call, which
         // needs 74 B of each ~800-B frame: those are gathered (mixed frames,
@@ -362,19 +398,8 @@ int frames_run_(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, 
         // 1.2 as DMA'd spans)
         // DMA only when the frames lie densely in the region (a slab of
         // frames): the spans are copied whole, gaps included
-        if (mode != M_RX) {
-            uintptr_t lo = ~(uintptr_t)0, hi = 0;
-            uint64_t sum = 0;
-            bool fits = true;
-            for (uint32_t i = 0; i < n; ++i) {
-                const uintptr_t a = (uintptr_t)fr[i].head;
-                lo = a < lo ? a : lo;
-                hi = a + fr[i].len > hi ? a + fr[i].len : hi;
-                sum += fr[i].len;
-                fits = fits && align16(fr[i].len + 15u) <= c->arena;
-            }
-            if (fits && hi - lo <= 2 * sum + (1ull << 20)) return frames_dma(c, *r, fr, n, mode, out, cb);
-        }
+        if (mode != M_RX && rs.fits && rs.hi - rs.lo <= 2 * rs.sum + (1ull << 20))
+            return frames_dma(c, *r, fr, n, mode, out, cb);
     }
     // scattered: every frame's slot offset (a prefix sum over the frames'
     // 16-B rounded need_len, in chunks on the pool threads); RX + L4 reads each

@@ -21,6 +21,8 @@
 #   txpmc                 FETCH_SIZE / WRITE_SIZE passes of the TX variants
 #   modes:K               K processes of scripts/lab_modes.py (mixed line modes)
 #   numa                  scripts/lab_numa.py (XCD <-> address-class locality probe)
+#   cputh, cputh_spin     scripts/lab_cpu_threads.py (host CPU time of the frame calls per thread;
+#                         _spin: LVLIP_BLOCK_MIN=0)
 #   window:SET            scripts/lab_window.py with LAB_SET=SET (read-order probes)
 #   evidence:WL           scripts/evidence.sh for WL (bench + trace + PMC of the kernel AUTO runs)
 #   pmc:WL                the PMC passes of that evidence alone (scripts/profile.sh)
@@ -68,6 +70,8 @@ for step in "$@"; do
       run txtrace 180 /opt/rocm/bin/rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/txpmc/trace \
         -o trace -- python3 scripts/lab_tx_store.py --only tx_product 20 ;;
     numa) run numa 300 python scripts/lab_numa.py "gpurun_out/${TAG}_numa.json" ;;
+    cputh) run cputh 300 python scripts/lab_cpu_threads.py "gpurun_out/${TAG}_cpu_threads.json" 40 ;;
+    cputh_spin) run cputh_spin 300 env LVLIP_BLOCK_MIN=0 python scripts/lab_cpu_threads.py "gpurun_out/${TAG}_cpu_threads_spin.json" 40 ;;
     window:*) set_=${step#window:}; run "window_$set_" 400 env LAB_SET="$set_" python scripts/lab_window.py "gpurun_out/${TAG}_window_$set_.json" ;;
     modes:*)
       k=${step#modes:}
