@@ -567,6 +567,7 @@ def run(args, world: int):
             diag["frames_dev"] = frames_dev(lvlip, torch, dev)
         if args.e2e:
             diag["e2e_host_GBps"] = e2e(lvlip, b, base)
+            diag["link_probe"] = link_probe(torch, dev, b.nbytes)
             diag["latency_us"] = latency(lvlip, torch, dev)
 
     cpu = None
@@ -713,6 +714,7 @@ def frames_dev(lvlip, torch, dev):
     end = int(fd["offset"][nh - 1]) + int(fd["len"][nh - 1])
     host = base[: (end + 15) // 16 * 16].cpu().numpy().copy()
     res["host"] = frames_host(lvlip, dev, host, fd[:nh], int(pay["len"][:nh].sum()))
+    res["host"]["link_probe"] = link_probe(torch, dev, host.nbytes)
     log("device-resident frames", res)
     return res
 
@@ -919,6 +921,42 @@ def read_probe(lvlip, torch, base, stream):
         best["window_c4"] = round(nb / ms / 1e6, 1)
     log("read_probe GB/s", best)
     return best
+
+
+def link_probe(torch, dev, nbytes):
+    """The host->device link's own rate, the ceiling of every host-resident
+    line (diagnostic): nbytes from pinned host memory to HBM as one copy, and
+    as 32 MiB copies back to back on one stream (the host pipelines' piece
+    size, csum_ctx.cpp kPieceMax), GB/s; each the best of 3."""
+    nbytes = min(int(nbytes), 1 << 31) & ~15
+    src = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    src.fill_(1)
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    piece = 32 << 20
+
+    def bulk():
+        dst.copy_(src, non_blocking=True)
+
+    def pieces():
+        for o in range(0, nbytes, piece):
+            dst[o:o + piece].copy_(src[o:o + piece], non_blocking=True)
+
+    res = {}
+    for name, fn in (("h2d_bulk", bulk), ("h2d_32MiB_pieces", pieces)):
+        fn()
+        stream.synchronize()
+        best = 0.0
+        for _ in range(3):
+            t0 = time.perf_counter()
+            fn()
+            stream.synchronize()
+            best = max(best, nbytes / (time.perf_counter() - t0) / 1e9)
+        res[name + "_GBps"] = round(best, 2)
+    res["bytes"] = nbytes
+    log("link probe", res)
+    del src, dst
+    return res
 
 
 def latency(lvlip, torch, dev):

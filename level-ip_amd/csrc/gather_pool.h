@@ -4,6 +4,7 @@
 // ASan on the CPU, without the HIP runtime.
 #pragma once
 
+#include <pthread.h>
 #include <stdint.h>
 
 #include <condition_variable>
@@ -68,6 +69,9 @@ class GatherPool {
 
    private:
     void worker(int id, uint64_t seen) {
+        // named, so per-thread CPU accounting (/proc/<pid>/task/*/comm) can
+        // tell the gather workers from the caller and the HIP runtime's threads
+        pthread_setname_np(pthread_self(), "lvlip-gather");
         std::unique_lock<std::mutex> g(m_);
         for (;;) {
             cv_job_.wait(g, [&] { return stop_ || gen_ != seen; });
