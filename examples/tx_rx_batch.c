@@ -16,7 +16,17 @@
  *      every 97th frame, and checks the verdicts.
  * Prints "tx_rx_batch ok ..." and exits 0 when everything matches.
  *
- *   make -C examples && examples/build/tx_rx_batch [frames]
+ * SOURCE picks where the frames live (INTEGRATION.md §2b''):
+ *   malloc    every frame its own malloc'd buffer, as level-ip allocates skbs
+ *             (src/skbuff.c:5-20): the library gathers them into its pinned arena
+ *   dma       every frame carved from one slab (64-B aligned, back to back)
+ *             registered once with LVLIP_REG_DMA: the copy engine reads the slab
+ *   zerocopy  the same slab registered LVLIP_REG_ZEROCOPY: the kernel reads it
+ *             in place over PCIe
+ * Each call's wall time and the process's CPU time per frame (every thread:
+ * the caller and the library's workers) are printed beside it.
+ *
+ *   make -C examples && examples/build/tx_rx_batch [frames] [malloc|dma|zerocopy]
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -43,14 +53,23 @@ static double now_ms(void)
     return t.tv_sec * 1e3 + t.tv_nsec / 1e6;
 }
 
+static double cpu_ms(void) /* the whole process: every thread */
+{
+    struct timespec t;
+    clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec / 1e6;
+}
+
 static void put16be(uint8_t *p, uint16_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
 
-/* one frame as ip_output leaves it (include/ip.h, include/tcp.h layouts) */
-static uint8_t *make_frame(uint32_t payload, uint32_t saddr, uint32_t daddr, uint32_t *flen)
+/* one frame as ip_output leaves it (include/ip.h, include/tcp.h layouts), in
+ * its own malloc'd buffer, or at *slab_at (advanced past it, 64-B aligned) */
+static uint8_t *make_frame(uint32_t payload, uint32_t saddr, uint32_t daddr, uint32_t *flen, uint8_t **slab_at)
 {
     const uint32_t iplen = 20 + 20 + payload;
-    uint8_t *h = malloc(14 + iplen);
+    uint8_t *h = slab_at ? *slab_at : malloc(14 + iplen);
     if (!h) return NULL;
+    if (slab_at) *slab_at += (14 + iplen + 63u) & ~63u;
     for (uint32_t i = 0; i < 14 + iplen; i++) h[i] = (uint8_t)rnd();
     put16be(h + 12, 0x0800);                 /* ethertype IPv4 */
     uint8_t *ih = h + 14;
@@ -69,15 +88,26 @@ static uint8_t *make_frame(uint32_t payload, uint32_t saddr, uint32_t daddr, uin
 int main(int argc, char **argv)
 {
     const uint32_t n = argc > 1 ? (uint32_t)strtoul(argv[1], NULL, 0) : 65536u;
+    const char *source = argc > 2 ? argv[2] : "malloc";
+    const int use_slab = strcmp(source, "malloc") != 0;
+    const uint32_t reg_flags = !strcmp(source, "zerocopy") ? LVLIP_REG_ZEROCOPY : LVLIP_REG_DMA;
+    if (use_slab && strcmp(source, "dma") && strcmp(source, "zerocopy")) {
+        fprintf(stderr, "usage: %s [frames] [malloc|dma|zerocopy]\n", argv[0]);
+        return 2;
+    }
     lvlip_frame *fr = calloc(n, sizeof *fr);
     uint8_t *verdict = malloc(n);
-    if (!fr || !verdict) return 2;
+    /* the slab: every frame's 64-B rounded size at most 14 + 40 + 1460 + 63 */
+    const size_t slab_bytes = use_slab ? (size_t)n * 1600u : 0;
+    uint8_t *slab_mem = use_slab ? malloc(slab_bytes + 64) : NULL;
+    uint8_t *slab = slab_mem ? (uint8_t *)(((uintptr_t)slab_mem + 63) & ~(uintptr_t)63) : NULL, *slab_at = slab;
+    if (!fr || !verdict || (use_slab && !slab)) return 2;
     for (uint32_t i = 0; i < n; i++) {
         /* 10.0.0.x <-> 10.0.0.y, and every 8th pair large enough that the
          * reference's u32 pseudo-header sum loses its carry (src/tcp.c:92-95) */
         const uint32_t a = (i % 8 == 0) ? 0xC8FFFFFFu : 0x0400000Au + (uint32_t)(rnd() % 200u) * 0x01000000u;
         const uint32_t b = (i % 8 == 0) ? 0x64FFFFFFu : 0x0500000Au;
-        fr[i].head = make_frame((uint32_t)(rnd() % 1461u), a, b, &fr[i].len);
+        fr[i].head = make_frame((uint32_t)(rnd() % 1461u), a, b, &fr[i].len, slab ? &slab_at : NULL);
         if (!fr[i].head) return 2;
     }
 
@@ -87,11 +117,15 @@ int main(int argc, char **argv)
         fprintf(stderr, "lvlip_csum_ctx_create: %s\n", lvlip_strerror(rc));
         return 1;
     }
+    if (slab && (rc = lvlip_csum_register(ctx, slab, slab_bytes, reg_flags)) != LVLIP_OK) {
+        fprintf(stderr, "lvlip_csum_register: %s\n", lvlip_strerror(rc));
+        return 1;
+    }
 
     /* 1. TX: every checksum of every frame in one batch */
-    double t0 = now_ms();
+    double t0 = now_ms(), c0 = cpu_ms();
     rc = lvlip_tx_checksum(ctx, fr, n);
-    const double tx_ms = now_ms() - t0;
+    const double tx_ms = now_ms() - t0, tx_cpu = cpu_ms() - c0;
     if (rc != LVLIP_OK) {
         fprintf(stderr, "lvlip_tx_checksum: %s\n", lvlip_strerror(rc));
         return 1;
@@ -130,8 +164,9 @@ int main(int argc, char **argv)
         corrupted++;
     }
     t0 = now_ms();
+    c0 = cpu_ms();
     rc = lvlip_rx_verify(ctx, fr, n, 0, verdict);
-    const double rx_ms = now_ms() - t0;
+    const double rx_ms = now_ms() - t0, rx_cpu = cpu_ms() - c0;
     if (rc != LVLIP_OK) {
         fprintf(stderr, "lvlip_rx_verify: %s\n", lvlip_strerror(rc));
         return 1;
@@ -144,10 +179,14 @@ int main(int argc, char **argv)
         fprintf(stderr, "RX: %u verdicts differ from ip_rcv's\n", bad);
         return 1;
     }
+    if (slab) (void)lvlip_csum_unregister(ctx, slab);
     lvlip_csum_ctx_destroy(ctx);
-    printf("tx_rx_batch ok: %u frames, TX fill %.2f ms, RX verify %.2f ms (%u corrupted frames dropped)\n",
-           n, tx_ms, rx_ms, corrupted);
-    for (uint32_t i = 0; i < n; i++) free(fr[i].head);
+    printf("tx_rx_batch ok: %u frames (%s), TX fill %.2f ms (%.0f ns CPU/frame), RX verify %.2f ms "
+           "(%.0f ns CPU/frame; %u corrupted frames dropped)\n",
+           n, source, tx_ms, tx_cpu * 1e6 / n, rx_ms, rx_cpu * 1e6 / n, corrupted);
+    if (slab) free(slab_mem);
+    else
+        for (uint32_t i = 0; i < n; i++) free(fr[i].head);
     free(fr);
     free(verdict);
     return 0;

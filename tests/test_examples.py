@@ -4,8 +4,9 @@ on the C ABI alone (built by __graft_entry__.build() / `make -C examples`).
 On the GPU it fills the TCP and IPv4 checksums of 65 536 level-ip frames in one
 call and checks every field against the per-call drop-in (tcp_v4_checksum's and
 ip_send_check's arithmetic, src/tcp.c:87-103, src/ip_output.c:8-12), then
-checks ip_rcv's verdicts for the same frames with every 97th one corrupted.
-Without a GPU it must fail loudly: there is no CPU fallback behind the batch
+checks ip_rcv's verdicts for the same frames with every 97th one corrupted,
+with the frames in malloc'd buffers and carved from one slab registered for
+DMA or for zero-copy reads (INTEGRATION.md §2b'').  Without a GPU it must fail loudly: there is no CPU fallback behind the batch
 calls."""
 import os
 import subprocess
@@ -33,11 +34,17 @@ def test_example_fails_loudly_without_gpu():
 
 
 @pytest.mark.gpu
-def test_example_tx_rx_batch():
+@pytest.mark.parametrize("source", ["malloc", "dma", "zerocopy"])
+def test_example_tx_rx_batch(source):
     assert os.path.exists(EXE), "examples/build/tx_rx_batch not built (run __graft_entry__.build())"
-    r = subprocess.run([EXE, "65536"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([EXE, "65536", source], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "tx_rx_batch ok: 65536 frames" in r.stdout, r.stdout
+    assert f"tx_rx_batch ok: 65536 frames ({source})" in r.stdout, r.stdout
+
+
+def test_example_rejects_unknown_source():
+    r = subprocess.run([_exe(), "64", "pinned"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr, (r.returncode, r.stderr)
 
 
 def test_install_and_build_against_it(tmp_path):
