@@ -942,8 +942,25 @@ def link_probe(torch, dev, nbytes):
         for o in range(0, nbytes, piece):
             dst[o:o + piece].copy_(src[o:o + piece], non_blocking=True)
 
+    # the host pipelines' shape: the pieces alternate over two streams (the
+    # context's two slots), each piece followed by a small copy (a piece's
+    # descriptors, 16 B per 1500-B packet)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    small = piece * 16 // 1504 & ~15
+
+    def two_streams(with_small=False):
+        for k, o in enumerate(range(0, nbytes, piece)):
+            with torch.cuda.stream(streams[k & 1]):
+                dst[o:o + piece].copy_(src[o:o + piece], non_blocking=True)
+                if with_small:
+                    dst[o:o + small].copy_(src[o:o + small], non_blocking=True)
+        for s in streams:
+            s.synchronize()
+
     res = {}
-    for name, fn in (("h2d_bulk", bulk), ("h2d_32MiB_pieces", pieces)):
+    for name, fn in (("h2d_bulk", bulk), ("h2d_32MiB_pieces", pieces),
+                     ("h2d_32MiB_pieces_2streams", two_streams),
+                     ("h2d_32MiB_pieces_2streams_desc", lambda: two_streams(True))):
         fn()
         stream.synchronize()
         best = 0.0
