@@ -68,13 +68,37 @@ int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes, uint6
     return LVLIP_OK;
 }
 
+// Two slots' copies issued on their own streams run side by side, share the
+// link and finish together; each slot's kernel and result copy then ran with
+// the link idle, 8.5 % of a registered batch's time (the pipeline's trace,
+// DESIGN.md §5).  On one copy stream the copies run back to back in issue
+// order, and each piece is summed and its results come back while the next
+// piece's copy runs.
+int h2d_ordered(lvlip_csum_ctx* c, Slot& s, void* dst, const void* src, size_t n, const char* what) {
+    hipError_t e;
+    if (!c->copy_order) {
+        if ((e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s.stream)) != hipSuccess)
+            return fail(c, e, what);
+        return LVLIP_OK;
+    }
+    // the slot's previous piece is drained (its kernel done) before the slot
+    // takes a new one, so the copy needs no wait of its own
+    if ((e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->copy_stream)) != hipSuccess)
+        return fail(c, e, what);
+    if ((e = hipEventRecord(s.copied, c->copy_stream)) != hipSuccess) return fail(c, e, "hipEventRecord");
+    if ((e = hipStreamWaitEvent(s.stream, s.copied, 0)) != hipSuccess) return fail(c, e, "hipStreamWaitEvent");
+    return LVLIP_OK;
+}
+
 int finish_pieces(lvlip_csum_ctx* c, int rc) {
     for (auto& s : c->slot) {
         const int r2 = drain(c, s);
         if (rc == LVLIP_OK) rc = r2;
     }
-    if (rc != LVLIP_OK)
+    if (rc != LVLIP_OK) {
         for (auto& s : c->slot) (void)hipStreamSynchronize(s.stream);
+        if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    }
     return rc;
 }
 
@@ -99,6 +123,7 @@ void free_slot(Slot& s) {
     if (s.d_desc) (void)hipFree(s.d_desc);
     if (s.d_out) (void)hipFree(s.d_out);
     if (s.done) (void)hipEventDestroy(s.done);
+    if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot{};
 }
@@ -123,15 +148,15 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
         if (rc != LVLIP_OK) return rc;
         return arm_slot(c, s, user_out, (size_t)count * sizeof(uint16_t), bytes);
     }
-    if (!dev_base) {
-        const uint64_t nb = src && src != s.h_bytes ? bytes : align16(bytes);
-        if ((e = hipMemcpyAsync(s.d_bytes, src ? src : s.h_bytes, nb, hipMemcpyHostToDevice,
-                                s.stream)) != hipSuccess)
-            return fail(c, e, "H2D bytes");
-    }
+    // the descriptors first: the bytes' copy may wait for the previous piece's
     if ((e = hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)count * sizeof(lvlip_csum_desc),
                             hipMemcpyHostToDevice, s.stream)) != hipSuccess)
         return fail(c, e, "H2D descriptors");
+    if (!dev_base) {
+        const uint64_t nb = src && src != s.h_bytes ? bytes : align16(bytes);
+        const int rc = h2d_ordered(c, s, s.d_bytes, src ? src : s.h_bytes, nb, "H2D bytes");
+        if (rc != LVLIP_OK) return rc;
+    }
     int rc = lvlip_csum_batch_dev_ex(dev_base ? dev_base : s.d_bytes, s.d_desc, count, s.d_out,
                                      s.stream, &cfg);
     if (rc != LVLIP_OK) return rc;
@@ -228,6 +253,10 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         c->block_min = v > 0 ? (uint64_t)v : 0u;
     }
     {
+        const char* e = getenv("LVLIP_COPY_ORDER");
+        c->copy_order = e ? atoi(e) != 0 : 1;
+    }
+    {
         const char* e = getenv("LVLIP_FRAME_TRACE");
         c->frame_trace = e && *e == '1';
     }
@@ -248,6 +277,7 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
             (e = hipMalloc((void**)&s.d_out, (size_t)c->max_desc * sizeof(uint16_t))) != hipSuccess ||
             (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&s.copied, hipEventDisableTiming)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&s.dh_bytes, s.h_bytes, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&s.dh_desc, s.h_desc, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&s.dh_out, s.h_out, 0)) != hipSuccess) {
@@ -257,6 +287,12 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
             return LVLIP_ENOMEM;
         }
     }
+    if (const hipError_t e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking); e != hipSuccess) {
+        fail(c, e, "lvlip_csum_ctx_create");
+        for (auto& t : c->slot) free_slot(t);
+        delete c;
+        return LVLIP_ENOMEM;
+    }
     *out = c;
     return LVLIP_OK;
 }
@@ -264,10 +300,12 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
 int lvlip_csum_ctx_destroy(lvlip_csum_ctx* c) {
     if (!c) return LVLIP_EINVAL;
     DeviceGuard g(c->device);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     for (auto& s : c->slot) {
         if (s.busy) (void)hipEventSynchronize(s.done);
         free_slot(s);
     }
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     for (const Region& r : c->regions) (void)hipHostUnregister(r.host);
     free(c->frame_scratch);
     free(c->frame_scratch2);

@@ -151,8 +151,10 @@ struct FrameSlots {
             const int r2 = drain_slot((next + j) % kSlots);
             if (rc == LVLIP_OK) rc = r2;
         }
-        if (rc != LVLIP_OK)
+        if (rc != LVLIP_OK) {
             for (auto& s : c->slot) (void)hipStreamSynchronize(s.stream);
+            if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+        }
         return rc;
     }
 };
@@ -173,15 +175,15 @@ int launch_frame_piece(lvlip_csum_ctx* c, Slot& s, int mode, uint64_t bytes, uin
         if (rc != LVLIP_OK) return rc;
         return arm_slot(c, s, user_out, nout, bytes);
     }
-    if (!dev_base) {
-        const uint64_t nb = src ? bytes : align16(bytes);
-        if ((e = hipMemcpyAsync(s.d_bytes, src ? src : s.h_bytes, nb, hipMemcpyHostToDevice, s.stream)) !=
-            hipSuccess)
-            return fail(c, e, "H2D frames");
-    }
+    // the descriptors first: the frames' copy may wait for the previous piece's
     if ((e = hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)k * sizeof(lvlip_frame_desc), hipMemcpyHostToDevice,
                             s.stream)) != hipSuccess)
         return fail(c, e, "H2D frame descriptors");
+    if (!dev_base) {
+        const uint64_t nb = src ? bytes : align16(bytes);
+        const int rc = h2d_ordered(c, s, s.d_bytes, src ? src : s.h_bytes, nb, "H2D frames");
+        if (rc != LVLIP_OK) return rc;
+    }
     const int rc = lvlip_frames_host_launch(mode, dev_base ? dev_base : s.d_bytes,
                                             (const lvlip_frame_desc*)s.d_desc, k, s.d_out, s.stream);
     if (rc != LVLIP_OK) return rc;

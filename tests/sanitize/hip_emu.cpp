@@ -64,6 +64,7 @@ hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
 }
 hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
 hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
 hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned int) {
     static char token;
     *e = (hipEvent_t)&token;
