@@ -8,7 +8,10 @@ The frames: bench.py's mixed frames (valid IPv4/TCP/ICMP, filled by the
 device TX call), a 512K-frame prefix copied to host memory as one slab, and
 the same frames scattered over 1616-B slots in random order.  Each config is
 a context created under its environment (LVLIP_FIRST_PIECE, LVLIP_PIECE_MAX,
-LVLIP_GATHER_THREADS); each call is timed (wall, 1 warm-up + 3)."""
+LVLIP_GATHER_THREADS, LVLIP_COPY_ORDER); each call is timed (wall, 1 warm-up
++ 3).  LAB_CONFIGS picks configs (comma list, default: all), LAB_SRC the
+sources (comma list of slab, scattered, dma: the slab registered
+LVLIP_REG_DMA; "all": slab and scattered; default scattered)."""
 import ctypes
 import json
 import os
@@ -25,6 +28,7 @@ CONFIGS = {
     "default": {},
     "t8": {"LVLIP_GATHER_THREADS": "8"},
     "noramp": {"LVLIP_FIRST_PIECE": str(32 << 20)},
+    "order0": {"LVLIP_COPY_ORDER": "0"},
 }
 
 
@@ -64,8 +68,13 @@ def main(out_path, rounds=3):
     hb = 20 * n + int(pay["len"][:n].sum())
     res = {}
     os.environ["LVLIP_FRAME_TRACE"] = "1"
+    names = os.environ.get("LAB_CONFIGS", ",".join(CONFIGS)).split(",")
+    srcs = os.environ.get("LAB_SRC", "scattered")
+    srcs = ["slab", "scattered"] if srcs == "all" else srcs.split(",")
+    arrs = {"slab": slab[1], "scattered": sc[1], "dma": slab[1]}
     for rnd in range(rounds):
-        for name, env in CONFIGS.items():
+        for name in names:
+            env = CONFIGS[name]
             for k, v in env.items():
                 os.environ[k] = v
             try:
@@ -73,8 +82,10 @@ def main(out_path, rounds=3):
             finally:
                 for k in env:
                     del os.environ[k]
-            for src, arr in (("scattered", sc[1]),) if os.environ.get("LAB_SRC") != "all" else \
-                    (("slab", slab[1]), ("scattered", sc[1])):
+            for src in srcs:
+                arr = arrs[src]
+                if src == "dma":
+                    ctx.register(host, lvlip.REG_DMA)
                 for call, fn in (("tx", lambda: lib.lvlip_tx_checksum(ctx._h, arr, n)),
                                  ("rx_l4", lambda: lib.lvlip_rx_verify(ctx._h, arr, n, 1, verdict.ctypes.data))):
                     assert fn() == 0
@@ -85,6 +96,8 @@ def main(out_path, rounds=3):
                     key = f"{name}/{src}/{call}"
                     res.setdefault(key, []).append(round(hb / ms / 1e6, 2))
                     print(key, res[key], file=sys.stderr, flush=True)
+                if src == "dma":
+                    ctx.unregister(host)
             ctx.close()
     with open(out_path, "w") as f:
         json.dump({"GBps_checksummed": res, "frames": n}, f, indent=1)
