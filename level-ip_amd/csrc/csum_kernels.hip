@@ -170,87 +170,8 @@ __global__ __launch_bounds__(256) void k_lane(const uint8_t* __restrict__ base,
     }
 }
 
-// ------------------------------------------ k_echo_reply (f4, RFC 1624) --
-//
-// icmpv4_reply (src/icmpv4.c:31-54) turns an echo request into the reply by
-// setting type 8 -> 0 and recomputing the ICMP checksum over the whole message
-// with the field zeroed (:45-47).  For a request whose checksum verified, the
-// reply's field follows from the request's field alone (RFC 1624 eqn. 3,
-// lvlip_icmp_echo_reply_csum in skb_batch.c): S = ~HC (0xffff
-// when HC = 0xffff, the other zero), S' = S + ~0x0008 with end-around carry,
-// field = ~S'.  S' = 0xffff cannot tell a zero-sum reply (field 0x0000) from
-// an all-zero one (field 0xffff); that frame's lane sums the message itself.
-// One lane per frame: the parse window (frame bytes [12, 56)) holds the IPv4
-// header and, for ihl <= 9, the ICMP type, code and checksum; nothing else of
-// the message is read except in the undecidable case.
-__device__ __forceinline__ uint32_t oc_add16(uint32_t a, uint32_t b) {
-    const uint32_t t = a + b;
-    return (t & 0xffffu) + (t >> 16);
-}
-
-// LVLIP_ECHO_FULL (icmpv4_reply's full sum for any request) is not this
-// kernel: it runs on the flat sweep with a frame source (FrameSrc<FR_ECHO>,
-// flat_src.h; round 5: 0.23 against 0.51 ms for one lane per frame summing
-// its message alone, 1M requests).
-__global__ __launch_bounds__(256) void k_echo_reply(uint8_t* __restrict__ base,
-                                                    const lvlip_frame_desc* __restrict__ frames,
-                                                    uint32_t n, uint8_t* __restrict__ status) {
-    const uint32_t f = blockIdx.x * 256u + threadIdx.x;
-    if (f >= n) return;  // no cross-lane step below
-    const uint4 raw = load_global(reinterpret_cast<uint64_t>(frames + f));
-    const uint64_t off = ((uint64_t)raw.y << 32) | raw.x;
-    const uint32_t len = raw.z;
-    uint8_t* h = base + off;
-    FrWin x;
-    x.load<4>(h, len, reinterpret_cast<uint64_t>(frames + f) & ~15ull);
-    uint32_t st = 0;
-    // the checks of lvlip_icmp_echo_reply_fill (skb_batch.c): an IPv4 ICMP echo
-    // request (type 8, code 0) whose message lies inside the frame
-    if (len >= FR_ETH + 20u) {
-        const uint32_t ver = x.b(14) >> 4, ihl = x.b(14) & 0x0fu, iplen = x.be16(16);
-        const uint32_t l4 = FR_ETH + ihl * 4u;
-        if (ver == 4u && ihl >= 5u && x.b(23) == 1u && iplen >= ihl * 4u + 4u && len >= FR_ETH + iplen) {
-            // type, code and checksum from the window when it holds them
-            // (ihl <= 9), else from memory
-            uint32_t type, code, hc;
-            if (l4 + 4u <= 56u) {
-                const uint32_t w = (ihl == 5u) ? x.le32(34) : (ihl == 6u) ? x.le32(38) : (ihl == 7u) ? x.le32(42)
-                                 : (ihl == 8u) ? x.le32(46) : x.le32(50);
-                type = w & 0xffu;
-                code = (w >> 8) & 0xffu;
-                hc = w >> 16;
-            } else {
-                type = h[l4];
-                code = h[l4 + 1u];
-                hc = fr_le16(h + l4 + 2u);
-            }
-            if (type == 8u && code == 0u) {
-                const uint32_t icmp_len = iplen - ihl * 4u;
-                const uint32_t S = hc == 0xffffu ? 0xffffu : (~hc & 0xffffu);
-                const uint32_t S1 = oc_add16(S, 0xffffu - 0x0008u);
-                uint32_t field;
-                if (S1 != 0xffffu) {
-                    field = ~S1 & 0xffffu;
-                    st = 1u;
-                } else {
-                    // src/icmpv4.c:45-47: type 0, field 0, checksum over icmp_len
-                    // bytes (words 0 and 1 are then zero)
-                    const uint8_t* m = h + l4;
-                    uint32_t acc = 0;
-                    uint32_t k = 4u;
-                    for (; k + 1u < icmp_len; k += 2u) acc += fr_le16(m + k);
-                    if (k < icmp_len) acc += m[k];
-                    field = finish(0u, acc);
-                    st = 2u;
-                }
-                h[l4] = 0u;  // ICMP_V4_REPLY
-                h[l4 + 2u] = (uint8_t)field;         // stored raw (no htons)
-                h[l4 + 3u] = (uint8_t)(field >> 8);
-            }
-        }
-    }
-    if (status) status[f] = (uint8_t)st;
-}
+// k_echo_reply (f4, RFC 1624) is in csum_dev.h, so that the lab library
+// can instantiate its store variants.
 }  // namespace lvlip
 
 // ======================================================== host side (C ABI) ==
@@ -648,13 +569,13 @@ int lvlip_icmp_echo_reply_dev_ex(void* base, const lvlip_frame_desc* frames, uin
         // one lane per frame summing its message alone ran 3-4x slower,
         // DESIGN.md §9)
         if (n > kMaxFrames * 2u) return LVLIP_EINVAL;
-        const int rc = lvlip::launch_frames_flat<lvlip::FR_ECHO, 8, 2>(base, frames, n, status, s, false);
+        const int rc = lvlip::launch_frames_flat<lvlip::FR_ECHO, 8, 2, 0, 0, lvlip::kEchoStore>(base, frames, n, status, s, false);
         if (rc == LVLIP_EHIP) return hip_fail(hipGetLastError(), "k_flat2 echo");
         return rc;
     }
     for (uint32_t f0 = 0; f0 < n;) {
         const uint32_t m = n - f0 < kLaunchMax ? n - f0 : kLaunchMax;
-        hipLaunchKernelGGL(lvlip::k_echo_reply, dim3((m + 255u) / 256u), dim3(256), 0, s,
+        hipLaunchKernelGGL(lvlip::k_echo_reply<lvlip::kEchoStore>, dim3((m + 255u) / 256u), dim3(256), 0, s,
                            (uint8_t*)base, frames + f0, m, status ? status + f0 : nullptr);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "k_echo_reply");

@@ -241,6 +241,25 @@ __device__ __forceinline__ void fr_store16_pol(uint64_t a, uint32_t c) {
 #undef LVLIP_ST
 }
 
+// An echo reply's type and checksum field at the message's first bytes m
+// (icmpv4_reply: type ICMP_V4_REPLY, src/icmpv4.c:45; the field stored raw,
+// :47).  STP 0: three byte stores (type, then the field's two bytes); 2-6:
+// two u16 stores with fr_store16_pol's policy, {type 0, code 0} then the
+// field (the request's code is 0: both callers checked it).
+template <int STP>
+__device__ __forceinline__ void fr_store_echo_reply(uint8_t* m, uint32_t field) {
+    if constexpr (STP == 0) {
+        m[0] = 0u;
+        m[2] = (uint8_t)field;
+        m[3] = (uint8_t)(field >> 8);
+    } else {
+        fr_store16_pol<STP>(reinterpret_cast<uint64_t>(m), 0u);
+        fr_store16_pol<STP>(reinterpret_cast<uint64_t>(m) + 2u, field & 0xffffu);
+    }
+}
+// The product's echo-reply stores (k_echo_reply, FrameSrc<FR_ECHO>).
+constexpr int kEchoStore = 0;
+
 // The decisions are those of skb_batch.c (host), which cites the reference line
 // of each.  Entry slots: RX with L4 and TX use two per frame (lanes 2f, 2f+1 of
 // one wave, so the pair exchanges results by shuffle), RX header-only one.  An
@@ -446,10 +465,7 @@ struct FrameSrc {
             if (!valid) return;
             uint32_t st = 0;
             if (w & 1u) {
-                uint8_t* p = wbase + (addr - reinterpret_cast<uint64_t>(base));
-                p[0] = 0u;
-                p[2] = (uint8_t)c;
-                p[3] = (uint8_t)(c >> 8);
+                fr_store_echo_reply<STP>(wbase + (addr - reinterpret_cast<uint64_t>(base)), c);
                 st = 2u;
             }
             if (out8) out8[f] = (uint8_t)st;

@@ -690,14 +690,31 @@ __attribute__((visibility("default"))) int lvlip_lab_batch_dev_ex(const void* ba
 // round, 4 block group order (else quarters), 8 block order with the frame
 // descriptors prefetched 1 280 tiles ahead (k_flat2's PFA); mode 0 alone: 16
 // / 32 the product's shape with whole 32-B / 64-B block field stores
-// (FrameSrc's SEC); mode 3: the prefetch distance (variant >> 3) x 160 blocks.
+// (FrameSrc's SEC); mode 3: the prefetch distance (variant >> 3) x 160 blocks;
+// modes 4 / 5: the echo reply with LVLIP_ECHO_FULL (the flat sweep) / from the
+// field (k_echo_reply), variant = the reply's store form (fr_store_echo_reply:
+// 0 three byte stores, 2-6 two u16 stores with that cache policy).
 __attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int variant, void* base,
                                                                 const lvlip_frame_desc* frames, uint32_t n,
                                                                 uint8_t* out8, void* stream) {
     if (n == 0) return LVLIP_OK;
     if (!base || !frames || n > LVLIP_MAX_BATCH / 2u || ((uintptr_t)base & 15u)) return LVLIP_EINVAL;
-    if (mode != 0 && !out8) return LVLIP_EINVAL;
+    if (mode != 0 && mode != 4 && mode != 5 && !out8) return LVLIP_EINVAL;
     hipStream_t s = (hipStream_t)stream;
+    if (mode == 4 || mode == 5) {
+        if (n > (1u << 30)) return LVLIP_EINVAL;  // one launch
+#define LVLIP_ECHO(P)                                                                                      \
+    case P:                                                                                                \
+        if (mode == 4) return lvlip::launch_frames_flat<lvlip::FR_ECHO, 8, 2, 0, 0, P>(base, frames, n, out8, s, false); \
+        hipLaunchKernelGGL(lvlip::k_echo_reply<P>, dim3((n + 255u) / 256u), dim3(256), 0, s, (uint8_t*)base,  \
+                           frames, n, out8);                                                               \
+        return hipGetLastError() == hipSuccess ? LVLIP_OK : LVLIP_EHIP;
+        switch (variant) {
+            LVLIP_ECHO(0) LVLIP_ECHO(2) LVLIP_ECHO(3) LVLIP_ECHO(4) LVLIP_ECHO(5) LVLIP_ECHO(6)
+            default: return LVLIP_EINVAL;
+        }
+#undef LVLIP_ECHO
+    }
     // TX fill with whole-block field stores (round 4): variant 16 = 32-B
     // sectors, 32 = 64-B blocks, on the product's shape (U 8, blocks;
     // nontemporal 16-B block stores; 2-B fields nontemporal)

@@ -548,8 +548,10 @@ def batch_host_flat_multi(ctxs, base: np.ndarray, descs: np.ndarray) -> np.ndarr
 def frames_variant_dev(mode: int, variant: int, base, fdescs, stream=None):
     """The frame calls' A/B variants (lvlip_lab_frames_dev, liblvlip_lab.so):
     mode 0 TX fill, 1 RX header on the flat sweep, 2 RX + L4; variant bits 1
-    plain field stores, 2 eight loads per round, 4 block order.  Returns the
-    per-frame status / verdict tensor."""
+    plain field stores, 2 eight loads per round, 4 block order; modes 4 / 5
+    the echo reply (LVLIP_ECHO_FULL / flags 0) with the reply's store form as
+    the variant (0 byte stores, 2-6 u16 stores with a cache policy).  Returns
+    the per-frame status / verdict tensor."""
     import torch
 
     n, fd = _frames_dev(base, fdescs)
