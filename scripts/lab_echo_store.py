@@ -3,7 +3,10 @@ lvlip_icmp_echo_reply_dev[_ex]) on the mixed config's 2M frames in HBM.
 Both reply kernels write the reply's type byte and checksum field into each
 request frame; fr_store_echo_reply (flat_src.h) does it as three byte stores
 (variant 0) or as two u16 stores with a cache policy (2 sc0, 3 sc1, 4 sc0 sc1,
-5 nt sc1, 6 nt sc0 sc1).  Modes: 4 = LVLIP_ECHO_FULL on the flat sweep, 5 =
+5 nt sc1, 6 nt sc0 sc1); for flags 0 also as one 16-B store of the patched
+window chunk (1 plain, 7 nontemporal; k_echo_reply's echo_reply_chunk_store).
+The first run (profiles/r05_echo_store.json) timed 0 and 2-6; this one 0, 2
+and the chunk stores.  Modes: 4 = LVLIP_ECHO_FULL on the flat sweep, 5 =
 flags 0 (k_echo_reply, the field from the request's field).  Each launch is
 timed alone with HIP events after the request bytes are restored, as
 bench.py's echo_reply_timing does; rounds interleave the variants.  Every
@@ -21,7 +24,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "level-ip_amd")]
 
-VARIANTS = (0, 6, 5, 4, 2)
+VARIANTS = {4: (0, 2), 5: (0, 2, 1, 7)}
 
 
 def main(path, rounds=5):
@@ -46,7 +49,7 @@ def main(path, rounds=5):
     res = {"frames": n, "icmp_frames": int(icmp.sum()), "icmp_bytes": msg_bytes, "parity": {}, "us": {}}
     for mode in (4, 5):
         want = None
-        for v in VARIANTS:
+        for v in VARIANTS[mode]:
             base.copy_(pristine)
             lvlip.frames_variant_dev(mode, v, base, fdt, stream=stream)
             torch.cuda.synchronize()
@@ -59,7 +62,7 @@ def main(path, rounds=5):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(rounds):
         for mode in (4, 5):
-            for v in VARIANTS:
+            for v in VARIANTS[mode]:
                 ts = []
                 for _ in range(5):
                     base[t_off] = 8
