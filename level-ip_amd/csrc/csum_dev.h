@@ -1203,38 +1203,6 @@ __device__ __forceinline__ uint32_t oc_add16(uint32_t a, uint32_t b) {
 // kernel: it runs on the flat sweep with a frame source (FrameSrc<FR_ECHO>,
 // flat_src.h; round 5: 0.23 against 0.51 ms for one lane per frame summing
 // its message alone, 1M requests).
-// The reply's type, code and field written as ONE 16-B store: the window
-// chunk that holds message bytes [0, 4), patched in registers (type 0, code 0,
-// the field raw), when that chunk lies inside the frame and the four bytes in
-// one chunk; otherwise three byte stores.  The rest of the chunk is rewritten
-// with the bytes loaded: only this lane writes inside its frame.  (Lab A/B,
-// k_echo_reply's STP 1 plain / 7 nontemporal)
-template <bool NT>
-__device__ __forceinline__ void echo_reply_chunk_store(uint8_t* h, uint32_t len, uint32_t l4, uint32_t field,
-                                                       const FrWin& x) {
-    const uint64_t m = reinterpret_cast<uint64_t>(h) + l4, c = m & ~15ull;
-    const uint32_t o = (uint32_t)(m & 15u), k = (uint32_t)((c - x.abase) >> 4);
-    if (o > 12u || c - x.abase > 48u || c + 16u > reinterpret_cast<uint64_t>(h) + len) {
-        fr_store_echo_reply<0>(h + l4, field);
-        return;
-    }
-    const uint4 q = k == 0u ? x.raw[0] : k == 1u ? x.raw[1] : k == 2u ? x.raw[2] : x.raw[3];
-    uint64_t lo = (uint64_t)q.x | ((uint64_t)q.y << 32), hi = (uint64_t)q.z | ((uint64_t)q.w << 32);
-    const uint64_t v = (uint64_t)(field & 0xffffu) << 16, msk = 0xffffffffull;  // bytes 0, 1 zero
-    if (o < 8u) {
-        lo = (lo & ~(msk << (8u * o))) | (v << (8u * o));
-        if (o > 4u) hi = (hi & ~(msk >> (64u - 8u * o))) | (v >> (64u - 8u * o));
-    } else {
-        hi = (hi & ~(msk << (8u * (o - 8u)))) | (v << (8u * (o - 8u)));
-    }
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const v4u w{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-    if constexpr (NT)
-        __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(c));
-    else
-        *reinterpret_cast<v4u*>(c) = w;
-}
-
 template <int STP>
 __global__ __launch_bounds__(256) void k_echo_reply(uint8_t* __restrict__ base,
                                                     const lvlip_frame_desc* __restrict__ frames,
@@ -1287,10 +1255,7 @@ __global__ __launch_bounds__(256) void k_echo_reply(uint8_t* __restrict__ base,
                     field = finish(0u, acc);
                     st = 2u;
                 }
-                if constexpr (STP == 1 || STP == 7)
-                    echo_reply_chunk_store<STP == 7>(h, len, l4, field, x);
-                else
-                    fr_store_echo_reply<STP>(h + l4, field);
+                fr_store_echo_reply<STP>(h + l4, field);
             }
         }
     }
