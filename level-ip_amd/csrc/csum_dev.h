@@ -1203,7 +1203,10 @@ __device__ __forceinline__ uint32_t oc_add16(uint32_t a, uint32_t b) {
 // kernel: it runs on the flat sweep with a frame source (FrameSrc<FR_ECHO>,
 // flat_src.h; round 5: 0.23 against 0.51 ms for one lane per frame summing
 // its message alone, 1M requests).
-template <int STP>
+// STP: the reply's store form (fr_store_echo_reply).  NCH: the parse window's
+// chunks, 4 (frame bytes [12, 56): ihl <= 9 from registers) or 3 ([12, 45)
+// at least: ihl <= 6, FrWin::load).
+template <int STP, int NCH = 4>
 __global__ __launch_bounds__(256) void k_echo_reply(uint8_t* __restrict__ base,
                                                     const lvlip_frame_desc* __restrict__ frames,
                                                     uint32_t n, uint8_t* __restrict__ status) {
@@ -1214,7 +1217,8 @@ __global__ __launch_bounds__(256) void k_echo_reply(uint8_t* __restrict__ base,
     const uint32_t len = raw.z;
     uint8_t* h = base + off;
     FrWin x;
-    x.load<4>(h, len, reinterpret_cast<uint64_t>(frames + f) & ~15ull);
+    x.load<NCH>(h, len, reinterpret_cast<uint64_t>(frames + f) & ~15ull);
+    constexpr uint32_t kWinEnd = NCH == 4 ? 56u : 45u;  // window bytes valid below this
     uint32_t st = 0;
     // the checks of lvlip_icmp_echo_reply_fill (skb_batch.c): an IPv4 ICMP echo
     // request (type 8, code 0) whose message lies inside the frame
@@ -1223,9 +1227,9 @@ __global__ __launch_bounds__(256) void k_echo_reply(uint8_t* __restrict__ base,
         const uint32_t l4 = FR_ETH + ihl * 4u;
         if (ver == 4u && ihl >= 5u && x.b(23) == 1u && iplen >= ihl * 4u + 4u && len >= FR_ETH + iplen) {
             // type, code and checksum from the window when it holds them
-            // (ihl <= 9), else from memory
+            // (ihl <= 9, or <= 6 with three chunks), else from memory
             uint32_t type, code, hc;
-            if (l4 + 4u <= 56u) {
+            if (l4 + 4u <= kWinEnd) {
                 const uint32_t w = (ihl == 5u) ? x.le32(34) : (ihl == 6u) ? x.le32(38) : (ihl == 7u) ? x.le32(42)
                                  : (ihl == 8u) ? x.le32(46) : x.le32(50);
                 type = w & 0xffu;

@@ -24,7 +24,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "level-ip_amd")]
 
-VARIANTS = {4: (0, 2), 5: (0, 2)}  # 1 / 7 (mode 5): the chunk store, last in commit 72b8c4f
+VARIANTS = {4: (0,), 5: (0, 8)}  # 1 / 7 (mode 5): the chunk store, last in commit 72b8c4f; 8: three-chunk window
 
 
 def main(path, rounds=5):
