@@ -6,6 +6,7 @@ the full 1 M x 1500 B / 1 M x 9000 B / 2 M-frame mixed batches, where every one
 of the N outputs is compared with the oracle run over the same bytes copied back
 from HBM.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -638,6 +639,48 @@ def test_host_direct_and_copied_pieces(monkeypatch, direct_max):
     with lvlip.Context(0, arena_bytes=1 << 20) as ctx:
         ctx.register(buf, lvlip.REG_ZEROCOPY)
         assert np.array_equal(ctx.batch_host_flat(buf, b.descs), want)
+
+
+@pytest.mark.parametrize("copy_order", ["0", "1"])
+def test_host_copy_order(monkeypatch, copy_order):
+    """LVLIP_COPY_ORDER (read when a context is made): 1 (the default) puts
+    every piece's H2D of its bytes on the context's one copy stream, the slot's
+    stream waiting for it; 0 issues it on the slot's stream.  Many small pieces
+    (a 256 KiB arena, no direct pieces) from the gather, a DMA region and the
+    iov path, and the frame calls from a DMA region: the same bits either way."""
+    monkeypatch.setenv("LVLIP_COPY_ORDER", copy_order)
+    monkeypatch.setenv("LVLIP_DIRECT_MAX", "0")
+    b = workloads.make("mixed", n=30000)
+    host = np.ascontiguousarray(b.host_bytes())
+    want = pyoracle.batch(host, b.descs, threads=THREADS)
+    with lvlip.Context(0, arena_bytes=256 << 10) as ctx:
+        assert np.array_equal(ctx.batch_host_flat(host, b.descs), want)
+        pk = [host[int(d["offset"]):int(d["offset"]) + max(int(d["len"]), 0)] for d in b.descs[:5000]]
+        st = [int(d["start_sum"]) for d in b.descs[:5000]]
+        assert np.array_equal(ctx.batch_host(pk, st), want[:5000])
+        ctx.register(host, lvlip.REG_DMA)
+        assert np.array_equal(ctx.batch_host_flat(host, b.descs), want)
+        ctx.unregister(host)
+    import skb_oracle
+
+    frames = workloads.frames(3000, seed=11)
+    ref = [bytearray(f) for f in frames]
+    for f in ref:
+        skb_oracle.tx_fill(f)
+    slab, fd = lvlip.pack_frames(frames, align_mod=16, seed=4)
+    with lvlip.Context(0, arena_bytes=256 << 10) as ctx:
+        ctx.register(slab, lvlip.REG_DMA)
+        arr = np.zeros(len(frames), dtype=[("head", "<u8"), ("len", "<u4"), ("pad", "<u4")])
+        arr["head"] = slab.ctypes.data + fd["offset"]
+        arr["len"] = fd["len"]
+        p = arr.ctypes.data_as(ctypes.POINTER(lvlip.Frame))
+        assert lvlip.lib().lvlip_tx_checksum(ctx._h, p, len(frames)) == 0
+        got = [slab[int(d["offset"]):int(d["offset"]) + int(d["len"])].tobytes() for d in fd]
+        assert got == [bytes(f) for f in ref]
+        verdict = np.zeros(len(frames), np.uint8)
+        assert lvlip.lib().lvlip_rx_verify(ctx._h, p, len(frames), 0, verdict.ctypes.data) == 0
+        assert verdict.tolist() == [skb_oracle.rx_verdict(f, 0) for f in ref]
+        ctx.unregister(slab)
 
 
 @pytest.mark.parametrize("direct_max", ["0", "1000000000000"])
