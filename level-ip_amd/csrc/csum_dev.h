@@ -1191,9 +1191,12 @@ namespace lvlip {
 // when HC = 0xffff, the other zero), S' = S + ~0x0008 with end-around carry,
 // field = ~S'.  S' = 0xffff cannot tell a zero-sum reply (field 0x0000) from
 // an all-zero one (field 0xffff); that frame's lane sums the message itself.
-// One lane per frame: the parse window (frame bytes [12, 56)) holds the IPv4
-// header and, for ihl <= 9, the ICMP type, code and checksum; nothing else of
-// the message is read except in the undecidable case.
+// One lane per frame: the parse window (the product's: three chunks, frame
+// bytes [12, 45) at least) holds the IPv4 header fields the checks read and,
+// for ihl <= 6, the ICMP type, code and checksum (longer headers: byte
+// loads); nothing else of the message is read except in the undecidable
+// case.  Three chunks against four: 119.8 against 126.7 us per 2M mixed
+// frames.
 __device__ __forceinline__ uint32_t oc_add16(uint32_t a, uint32_t b) {
     const uint32_t t = a + b;
     return (t & 0xffffu) + (t >> 16);

@@ -575,7 +575,7 @@ int lvlip_icmp_echo_reply_dev_ex(void* base, const lvlip_frame_desc* frames, uin
     }
     for (uint32_t f0 = 0; f0 < n;) {
         const uint32_t m = n - f0 < kLaunchMax ? n - f0 : kLaunchMax;
-        hipLaunchKernelGGL(lvlip::k_echo_reply<lvlip::kEchoStore>, dim3((m + 255u) / 256u), dim3(256), 0, s,
+        hipLaunchKernelGGL((lvlip::k_echo_reply<lvlip::kEchoStore, 3>), dim3((m + 255u) / 256u), dim3(256), 0, s,
                            (uint8_t*)base, frames + f0, m, status ? status + f0 : nullptr);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "k_echo_reply");

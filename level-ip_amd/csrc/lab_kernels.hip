@@ -695,7 +695,8 @@ __attribute__((visibility("default"))) int lvlip_lab_batch_dev_ex(const void* ba
 // field (k_echo_reply), variant = the reply's store form (fr_store_echo_reply:
 // 0 three byte stores, 2-6 two u16 stores with that cache policy; the
 // patched 16-B window chunk of flags 0 was measured and removed, last in
-// commit 72b8c4f); mode 5 variant 8: byte stores with a three-chunk window.
+// commit 72b8c4f); mode 5 variant 8: byte stores with a three-chunk window
+// (the product's since round 5), variant 0 etc. the four-chunk window.
 __attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int variant, void* base,
                                                                 const lvlip_frame_desc* frames, uint32_t n,
                                                                 uint8_t* out8, void* stream) {
@@ -711,7 +712,7 @@ __attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int va
         hipLaunchKernelGGL(lvlip::k_echo_reply<P>, dim3((n + 255u) / 256u), dim3(256), 0, s, (uint8_t*)base,  \
                            frames, n, out8);                                                               \
         return hipGetLastError() == hipSuccess ? LVLIP_OK : LVLIP_EHIP;
-        if (mode == 5 && variant == 8) {  // byte stores, a three-chunk parse window
+        if (mode == 5 && variant == 8) {  // byte stores, a three-chunk parse window (the product)
             hipLaunchKernelGGL((lvlip::k_echo_reply<0, 3>), dim3((n + 255u) / 256u), dim3(256), 0, s,
                                (uint8_t*)base, frames, n, out8);
             return hipGetLastError() == hipSuccess ? LVLIP_OK : LVLIP_EHIP;
