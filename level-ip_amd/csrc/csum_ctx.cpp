@@ -16,6 +16,7 @@
 #include <string.h>
 #include <time.h>
 
+#include <atomic>
 #include <string>
 #include <thread>
 #include <vector>
@@ -166,12 +167,38 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
     return arm_slot(c, s, user_out, (size_t)count * sizeof(uint16_t), bytes);
 }
 
+// The code of the first item (in batch order) that `check` refuses, or
+// LVLIP_OK, checked on the pool threads: the host calls' up-front passes over
+// a whole batch ran on the calling thread before the first piece, 1-2 ms per
+// 1M descriptors with the link idle.
+template <class F>
+int first_failure(lvlip_csum_ctx* c, uint32_t n, const F& check) {
+    std::atomic<uint64_t> first{~0ull};  // (item << 8) | -code of the earliest refusal seen
+    parallel_ranges(c, n, 65536, [&first, &check](uint64_t lo, uint64_t hi) {
+        for (uint64_t q = lo; q < hi; ++q) {
+            const int r = check((uint32_t)q);
+            if (r == LVLIP_OK) continue;
+            const uint64_t key = (q << 8) | (uint64_t)(-r);
+            uint64_t cur = first.load(std::memory_order_relaxed);
+            while (key < cur && !first.compare_exchange_weak(cur, key, std::memory_order_relaxed)) {
+            }
+            return;  // the rest of this range comes later in batch order
+        }
+    });
+    const uint64_t f = first.load(std::memory_order_relaxed);
+    return f == ~0ull ? LVLIP_OK : -(int)(f & 0xffu);
+}
+
 // Zero-copy: descriptors only (offsets from the region's first byte rounded
 // down to 16), kernel reads the registered pages in place.  `offset_of(i)`
-// gives packet i's byte address; the whole batch lies in region `r`.
-template <class AddrOf, class DescOf>
+// gives packet i's byte address; the whole batch lies in region `r`.  Pieces
+// of at most c->piece bytes (the descriptors of the next piece are written,
+// on the pool threads, while the kernel reads the previous one's packets;
+// a piece was max_desc descriptors before, for a 1M-packet batch one piece
+// whose 16 MB of descriptors were written before the kernel started).
+template <class AddrOf, class DescOf, class LenOf>
 int zerocopy_batch(lvlip_csum_ctx* c, const Region& r, uint32_t n, uint16_t* out, AddrOf addr_of,
-                   DescOf desc_of) {
+                   DescOf desc_of, LenOf len_of) {
     const uint8_t* h0 = (const uint8_t*)((uintptr_t)r.host & ~(uintptr_t)15);
     const uint8_t* d0 = r.dev - (r.host - h0);
     int cur = 0;
@@ -181,15 +208,24 @@ int zerocopy_batch(lvlip_csum_ctx* c, const Region& r, uint32_t n, uint16_t* out
         Slot& s = c->slot[cur];
         if ((rc = drain(c, s)) != LVLIP_OK) break;
         const uint32_t first = i;
-        const uint32_t k = n - i < c->max_desc ? n - i : c->max_desc;
+        uint32_t k = 0;
         uint64_t bytes = 0;
-        for (uint32_t q = 0; q < k; ++q) {
-            lvlip_csum_desc dq = desc_of(first + q);
-            dq.offset = (uint64_t)((const uint8_t*)addr_of(first + q) - h0);
-            bytes += dq.len > 0 ? (uint64_t)dq.len : 0u;
-            s.h_desc[q] = dq;
+        while (i < n && k < c->max_desc) {
+            const int32_t l = len_of(i);
+            const uint64_t need = l > 0 ? (uint64_t)l : 0u;
+            if (k && bytes + need > c->piece) break;
+            bytes += need;
+            ++k;
+            ++i;
         }
-        i += k;
+        lvlip_csum_desc* hd = s.h_desc;
+        parallel_ranges(c, k, 16384, [&, hd, first](uint64_t lo, uint64_t hi) {
+            for (uint64_t q = lo; q < hi; ++q) {
+                lvlip_csum_desc dq = desc_of(first + (uint32_t)q);
+                dq.offset = (uint64_t)((const uint8_t*)addr_of(first + (uint32_t)q) - h0);
+                hd[q] = dq;
+            }
+        });
         rc = launch_piece(c, s, bytes ? bytes : 16, k, out + first, nullptr, d0);
         cur ^= 1;
     }
@@ -360,20 +396,22 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
                           uint16_t* out) {
     if (!c || (n && (!pkts || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
-    for (uint32_t i = 0; i < n; ++i)
-        if (pkts[i].len > 0 && !pkts[i].ptr) return LVLIP_EINVAL;
+    if (first_failure(c, n, [pkts](uint32_t i) { return pkts[i].len > 0 && !pkts[i].ptr ? LVLIP_EINVAL : LVLIP_OK; }) !=
+        LVLIP_OK)
+        return LVLIP_EINVAL;
     DeviceGuard g(c->device);
     if (!c->regions.empty()) {
-        // f3: all packets inside one zero-copy region -> no gather at all
-        const Region* r = nullptr;
-        uint32_t i = 0;
-        for (; i < n; ++i) {
-            if (pkts[i].len <= 0) continue;
-            const Region* ri = find_region(c, pkts[i].ptr, (uint64_t)pkts[i].len);
-            if (!ri || !(ri->flags & LVLIP_REG_ZEROCOPY) || (r && ri != r)) break;
-            r = ri;
-        }
-        if (i == n && r)
+        // f3: all packets inside one zero-copy region -> no gather at all (the
+        // region of the first non-empty packet; regions never overlap)
+        uint32_t i0 = 0;
+        while (i0 < n && pkts[i0].len <= 0) ++i0;
+        const Region* r = i0 < n ? find_region(c, pkts[i0].ptr, (uint64_t)pkts[i0].len) : nullptr;
+        if (r && (r->flags & LVLIP_REG_ZEROCOPY) &&
+            first_failure(c, n, [pkts, r](uint32_t q) {
+                const uint8_t* a = (const uint8_t*)pkts[q].ptr;
+                return pkts[q].len <= 0 || (a >= r->host && a + pkts[q].len <= r->host + r->bytes) ? LVLIP_OK
+                                                                                                  : LVLIP_EINVAL;
+            }) == LVLIP_OK)
             return zerocopy_batch(
                 c, *r, n, out,
                 [&](uint32_t q) { return pkts[q].len > 0 ? (const uint8_t*)pkts[q].ptr : r->host; },
@@ -382,11 +420,14 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
                     d.len = pkts[q].len;
                     d.start_sum = pkts[q].start_sum;
                     return d;
-                });
+                },
+                [&](uint32_t q) { return pkts[q].len; });
     }
-    for (uint32_t i = 0; i < n; ++i)
-        if (pkts[i].len > 0 && align16((uint64_t)pkts[i].len) > c->arena)
-            return LVLIP_ERANGE;  // a single packet larger than the arena
+    const uint64_t arena = c->arena;
+    if (first_failure(c, n, [pkts, arena](uint32_t i) {
+            return pkts[i].len > 0 && align16((uint64_t)pkts[i].len) > arena ? LVLIP_ERANGE : LVLIP_OK;
+        }) != LVLIP_OK)
+        return LVLIP_ERANGE;  // a single packet larger than the arena
 
     int cur = 0;
     uint32_t i = 0;
@@ -436,19 +477,22 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
     if (!c || (n && (!base || !d || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
     const uint8_t* b = (const uint8_t*)base;
-    for (uint32_t q = 0; q < n; ++q) {
+    const uint64_t arena = c->arena;
+    const int bad = first_failure(c, n, [d, base_bytes, arena](uint32_t q) {
         const uint64_t e = d[q].offset + (d[q].len > 0 ? (uint64_t)d[q].len : 0u);
         if (e > base_bytes) return LVLIP_EINVAL;
         // a single packet whose 16-B span exceeds the arena: refuse before any
         // piece is in flight (a piece still in flight would later write into out[])
-        if (align16(e) - (d[q].offset & ~15ull) > c->arena) return LVLIP_ERANGE;
-    }
+        if (align16(e) - (d[q].offset & ~15ull) > arena) return LVLIP_ERANGE;
+        return LVLIP_OK;
+    });
+    if (bad != LVLIP_OK) return bad;
     DeviceGuard g(c->device);
     const Region* reg = c->regions.empty() ? nullptr : find_region(c, b, base_bytes);
     if (reg && (reg->flags & LVLIP_REG_ZEROCOPY))
         return zerocopy_batch(
             c, *reg, n, out, [&](uint32_t q) { return b + d[q].offset; },
-            [&](uint32_t q) { return d[q]; });
+            [&](uint32_t q) { return d[q]; }, [&](uint32_t q) { return d[q].len; });
 
     int cur = 0;
     uint32_t i = 0;
@@ -492,9 +536,16 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
                 _mm_sfence();
             });
         }
-        for (uint32_t q = 0; q < k; ++q) {
-            s.h_desc[q] = d[first + q];
-            s.h_desc[q].offset = d[first + q].offset - lo16;
+        {
+            lvlip_csum_desc* hd = s.h_desc;
+            const lvlip_csum_desc* src = d + first;
+            const uint64_t base16 = lo16;
+            parallel_ranges(c, k, 16384, [hd, src, base16](uint64_t lo, uint64_t hi) {
+                for (uint64_t q = lo; q < hi; ++q) {
+                    hd[q] = src[q];
+                    hd[q].offset = src[q].offset - base16;
+                }
+            });
         }
         rc = launch_piece(c, s, span ? span : 16, k, out + first, from);
         cur ^= 1;
