@@ -1,0 +1,92 @@
+"""Lab (diagnostic, not the product): two builds of the product library in one
+process, on the host-resident batch calls (lvlip_csum_batch_host_flat from
+plain memory, from a LVLIP_REG_DMA and a LVLIP_REG_ZEROCOPY region, and
+lvlip_csum_batch_host over an iov array), rounds interleaved.  The second
+build is a library built from an earlier commit and placed at
+level-ip_amd/build/prev/liblvlip_csum.so (git-ignored; it travels to the GPU
+box with the tree):
+
+    git worktree add /tmp/prev <commit> && make -C /tmp/prev/level-ip_amd \\
+        /tmp/prev/level-ip_amd/liblvlip_csum.so
+    mkdir -p level-ip_amd/build/prev && cp /tmp/prev/level-ip_amd/liblvlip_csum.so level-ip_amd/build/prev/
+    python scripts/lab_lib_ab.py OUT.json [WORKLOAD] [ROUNDS]
+
+Both libraries are driven through their C ABI only (ctypes); every call's
+outputs are compared with the first call's.
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "level-ip_amd")]
+
+
+def bind(path):
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    lib.lvlip_csum_ctx_create.argtypes = [ctypes.POINTER(vp), i32, ctypes.c_size_t]
+    lib.lvlip_csum_ctx_destroy.argtypes = [vp]
+    lib.lvlip_csum_register.argtypes = [vp, vp, ctypes.c_size_t, u32]
+    lib.lvlip_csum_unregister.argtypes = [vp, vp]
+    lib.lvlip_csum_batch_host_flat.argtypes = [vp, vp, ctypes.c_size_t, vp, u32, vp]
+    lib.lvlip_csum_batch_host.argtypes = [vp, vp, u32, vp]
+    return lib
+
+
+def main(path, workload="tcp1500", rounds=3, reps=3):
+    import lvlip
+    import workloads
+
+    libs = {"cur": bind(lvlip.LIB_PATH),
+            "prev": bind(os.path.join(ROOT, "level-ip_amd", "build", "prev", "liblvlip_csum.so"))}
+    b = workloads.make(workload)
+    host = np.ascontiguousarray(b.host_bytes())
+    d = np.ascontiguousarray(b.descs, dtype=lvlip.DESC_DTYPE)
+    iov = np.zeros(b.n, dtype=[("ptr", "<u8"), ("len", "<i4"), ("start_sum", "<u4")])
+    iov["ptr"] = host.ctypes.data + d["offset"]
+    iov["len"] = d["len"]
+    iov["start_sum"] = d["start_sum"]
+    out = np.empty(b.n, np.uint16)
+    want = None
+    res = {"workload": workload, "GBps": {}}
+    for _ in range(rounds):
+        for name, lib in libs.items():
+            for src in ("gather", "dma", "zerocopy", "iov"):
+                h = ctypes.c_void_p()
+                assert lib.lvlip_csum_ctx_create(ctypes.byref(h), 0, 256 << 20) == 0
+                if src in ("dma", "zerocopy"):
+                    flag = lvlip.REG_DMA if src == "dma" else lvlip.REG_ZEROCOPY
+                    assert lib.lvlip_csum_register(h, host.ctypes.data, host.size, flag) == 0
+                if src == "iov":
+                    def call():
+                        return lib.lvlip_csum_batch_host(h, iov.ctypes.data, b.n, out.ctypes.data)
+                else:
+                    def call():
+                        return lib.lvlip_csum_batch_host_flat(h, host.ctypes.data, host.size, d.ctypes.data, b.n,
+                                                              out.ctypes.data)
+                assert call() == 0
+                if want is None:
+                    want = out.copy()
+                assert np.array_equal(out, want), (name, src)
+                best = 0.0
+                for _ in range(reps):
+                    t0 = time.perf_counter()
+                    assert call() == 0
+                    best = max(best, b.algo_bytes / (time.perf_counter() - t0) / 1e9)
+                assert np.array_equal(out, want), (name, src)
+                lib.lvlip_csum_ctx_destroy(h)
+                key = f"{name} {src}"
+                res["GBps"].setdefault(key, []).append(round(best, 2))
+                print(key, res["GBps"][key], flush=True)
+    with open(path, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "tcp1500",
+         int(sys.argv[3]) if len(sys.argv) > 3 else 3)
