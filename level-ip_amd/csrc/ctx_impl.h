@@ -105,7 +105,7 @@ int h2d_ordered(lvlip_csum_ctx* c, Slot& s, void* dst, const void* src, size_t n
 // Waits for a slot's in-flight piece and copies its results to user_out.
 int drain(lvlip_csum_ctx* c, Slot& s);
 // End of a batch call: drains both slots; after a failure also waits for what
-// a half-enqueued piece left on the slot streams.
+// a half-enqueued piece left on the slot streams and the copy stream.
 int finish_pieces(lvlip_csum_ctx* c, int rc);
 // The registered region holding [p, p + len), or nullptr.
 const Region* find_region(const lvlip_csum_ctx* c, const void* p, uint64_t len);
