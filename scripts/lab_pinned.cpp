@@ -2,6 +2,7 @@
 // against malloc'd memory, one thread: big memcpy in, sequential reads, and the
 // frame gather's pattern (40K ~800-B copies into 16-B slots, slot offsets read
 // from a descriptor array in pinned or in malloc'd memory).
+//   hipcc -O2 -std=c++17 -o scripts/lab_pinned scripts/lab_pinned.cpp   (git-ignored)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
