@@ -494,6 +494,10 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
             c, *reg, n, out, [&](uint32_t q) { return b + d[q].offset; },
             [&](uint32_t q) { return d[q]; }, [&](uint32_t q) { return d[q].len; });
 
+    // a piece's bytes: from a DMA region the whole arena (no gather to
+    // overlap with the copies, and each copy costs the copy engine ~18 us
+    // between pieces: DESIGN.md §5), else LVLIP_PIECE_MAX
+    const uint64_t limit = reg ? c->arena : c->piece;
     int cur = 0;
     uint32_t i = 0;
     int rc = LVLIP_OK;
@@ -512,7 +516,7 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
             const uint64_t nlo = (o & ~15ull) < lo16 ? (o & ~15ull) : lo16;
             const uint64_t nhi = e > hi ? e : hi;
             // k >= 1 here: a single span always fits the arena (checked above)
-            if (align16(nhi) - nlo > (k ? c->piece : c->arena)) break;
+            if (align16(nhi) - nlo > (k ? limit : c->arena)) break;
             lo16 = nlo;
             hi = nhi;
             ++k;

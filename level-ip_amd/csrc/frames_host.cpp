@@ -315,6 +315,9 @@ int frames_dma(lvlip_csum_ctx* c, const Region& r, const lvlip_frame* fr, uint32
         const uint32_t first = i;
         uintptr_t lo = ~(uintptr_t)0, hi = 0;
         uint32_t k = 0;
+        // (pieces grown to the whole arena, as the flat host call's DMA pieces,
+        // lost here: TX's last piece's field stores no longer overlap a copy;
+        // DESIGN.md §9)
         const uint64_t pb = piece_bytes(c, idx++);
         while (i < n && k < fmax) {
             const uintptr_t a = (uintptr_t)fr[i].head, e = a + fr[i].len;

@@ -10,6 +10,9 @@ box with the tree):
         /tmp/prev/level-ip_amd/liblvlip_csum.so
     mkdir -p level-ip_amd/build/prev && cp /tmp/prev/level-ip_amd/liblvlip_csum.so level-ip_amd/build/prev/
     python scripts/lab_lib_ab.py OUT.json [WORKLOAD] [ROUNDS]
+    python scripts/lab_lib_ab.py OUT.json frames [ROUNDS]   # the host frame calls
+
+LAB_ARENA sets the contexts' arena bytes (default 256 MiB, as bench.py --e2e).
 
 Both libraries are driven through their C ABI only (ctypes); every call's
 outputs are compared with the first call's.
@@ -35,7 +38,59 @@ def bind(path):
     lib.lvlip_csum_unregister.argtypes = [vp, vp]
     lib.lvlip_csum_batch_host_flat.argtypes = [vp, vp, ctypes.c_size_t, vp, u32, vp]
     lib.lvlip_csum_batch_host.argtypes = [vp, vp, u32, vp]
+    lib.lvlip_tx_checksum.argtypes = [vp, vp, u32]
+    lib.lvlip_rx_verify.argtypes = [vp, vp, u32, u32, vp]
     return lib
+
+
+def frames_ab(path, libs, rounds, arena, reps=3):
+    """The host frame calls (TX fill, RX + L4) on 512K of bench.py's mixed
+    frames in host memory, from a plain slab and from the slab registered
+    LVLIP_REG_DMA, per library."""
+    import torch
+
+    import bench
+    import lvlip
+
+    dev = torch.device("cuda", 0)
+    base, fd, pay = bench.mixed_frames_hbm(lvlip, torch, dev)
+    fdt = torch.from_numpy(fd.view(np.uint8).copy()).to(dev)
+    lvlip.tx_checksum_dev(base, fdt)
+    torch.cuda.synchronize()
+    n = min(fd.size, 1 << 19)
+    end = int(fd["offset"][n - 1]) + int(fd["len"][n - 1])
+    host = base[: (end + 15) // 16 * 16].cpu().numpy().copy()
+    del base, fdt
+    fr = np.zeros(n, dtype=[("head", "<u8"), ("len", "<u4"), ("pad", "<u4")])
+    fr["head"] = host.ctypes.data + fd["offset"][:n].astype(np.uint64)
+    fr["len"] = fd["len"][:n]
+    hb = 20 * n + int(pay["len"][:n].sum())
+    verdict = np.zeros(n, np.uint8)
+    want = host.copy()
+    res = {"frames": n, "arena": arena, "GBps": {}}
+    for _ in range(rounds):
+        for name, lib in libs.items():
+            for src in ("slab", "dma"):
+                h = ctypes.c_void_p()
+                assert lib.lvlip_csum_ctx_create(ctypes.byref(h), 0, arena) == 0
+                if src == "dma":
+                    assert lib.lvlip_csum_register(h, host.ctypes.data, host.size, lvlip.REG_DMA) == 0
+                for call, fn in (("tx", lambda: lib.lvlip_tx_checksum(h, fr.ctypes.data, n)),
+                                 ("rx_l4", lambda: lib.lvlip_rx_verify(h, fr.ctypes.data, n, lvlip.RX_VERIFY_L4,
+                                                                       verdict.ctypes.data))):
+                    assert fn() == 0
+                    best = 0.0
+                    for _ in range(reps):
+                        t0 = time.perf_counter()
+                        assert fn() == 0
+                        best = max(best, hb / (time.perf_counter() - t0) / 1e9)
+                    key = f"{name} {src} {call}"
+                    res["GBps"].setdefault(key, []).append(round(best, 2))
+                    print(key, res["GBps"][key], flush=True)
+                assert np.array_equal(host, want), (name, src)  # the TX fill is idempotent
+                lib.lvlip_csum_ctx_destroy(h)
+    with open(path, "w") as f:
+        json.dump(res, f, indent=1)
 
 
 def main(path, workload="tcp1500", rounds=3, reps=3):
@@ -44,6 +99,9 @@ def main(path, workload="tcp1500", rounds=3, reps=3):
 
     libs = {"cur": bind(lvlip.LIB_PATH),
             "prev": bind(os.path.join(ROOT, "level-ip_amd", "build", "prev", "liblvlip_csum.so"))}
+    arena = int(os.environ.get("LAB_ARENA", 256 << 20))
+    if workload == "frames":
+        return frames_ab(path, libs, rounds, arena)
     b = workloads.make(workload)
     host = np.ascontiguousarray(b.host_bytes())
     d = np.ascontiguousarray(b.descs, dtype=lvlip.DESC_DTYPE)
@@ -53,12 +111,12 @@ def main(path, workload="tcp1500", rounds=3, reps=3):
     iov["start_sum"] = d["start_sum"]
     out = np.empty(b.n, np.uint16)
     want = None
-    res = {"workload": workload, "GBps": {}}
+    res = {"workload": workload, "arena": arena, "GBps": {}}
     for _ in range(rounds):
         for name, lib in libs.items():
             for src in ("gather", "dma", "zerocopy", "iov"):
                 h = ctypes.c_void_p()
-                assert lib.lvlip_csum_ctx_create(ctypes.byref(h), 0, 256 << 20) == 0
+                assert lib.lvlip_csum_ctx_create(ctypes.byref(h), 0, arena) == 0
                 if src in ("dma", "zerocopy"):
                     flag = lvlip.REG_DMA if src == "dma" else lvlip.REG_ZEROCOPY
                     assert lib.lvlip_csum_register(h, host.ctypes.data, host.size, flag) == 0
