@@ -255,6 +255,28 @@ int main() {
     CHECK(lvlip_csum_batch_host(ctx, nullptr, 0, nullptr) == LVLIP_OK, "n = 0");
     lvlip_csum_desc bad{10, 20, 0};
     CHECK(lvlip_csum_batch_host_flat(ctx, big.data(), 25, &bad, 1, &o) == LVLIP_EINVAL, "flat bounds");
+    // the up-front checks run on the pool threads over ranges of the batch
+    // (first_failure): the refusal is still the first bad descriptor's, in
+    // batch order, whichever thread sees which (n spans several ranges)
+    {
+        const uint32_t n = 400000;
+        std::vector<lvlip_csum_desc> d(n, lvlip_csum_desc{0, 64, 0});
+        std::vector<uint16_t> out(n);
+        lvlip_csum_desc past{big.size() - 8, 16, 0};              // past base_bytes: EINVAL
+        lvlip_csum_desc huge{0, (int32_t)(big.size() - 16), 0};  // span > the 1 MiB arena: ERANGE
+        d[300001] = past;
+        d[350002] = huge;
+        CHECK(lvlip_csum_batch_host_flat(ctx, big.data(), big.size(), d.data(), n, out.data()) == LVLIP_EINVAL,
+              "first bad descriptor EINVAL");
+        d[100003] = huge;
+        CHECK(lvlip_csum_batch_host_flat(ctx, big.data(), big.size(), d.data(), n, out.data()) == LVLIP_ERANGE,
+              "first bad descriptor ERANGE");
+        std::vector<lvlip_csum_iov> iov(n, lvlip_csum_iov{big.data(), 64, 0});
+        iov[200000] = lvlip_csum_iov{nullptr, 8, 0};
+        CHECK(lvlip_csum_batch_host(ctx, iov.data(), n, out.data()) == LVLIP_EINVAL, "null iov refused");
+        iov[200000] = one;
+        CHECK(lvlip_csum_batch_host(ctx, iov.data(), n, out.data()) == LVLIP_ERANGE, "oversize iov refused");
+    }
 
     // a region left registered is released by destroy
     uint8_t* left = (uint8_t*)malloc(1u << 16);
