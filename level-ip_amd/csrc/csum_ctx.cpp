@@ -213,7 +213,7 @@ int zerocopy_batch(lvlip_csum_ctx* c, const Region& r, uint32_t n, uint16_t* out
         while (i < n && k < c->max_desc) {
             const int32_t l = len_of(i);
             const uint64_t need = l > 0 ? (uint64_t)l : 0u;
-            if (k && bytes + need > c->piece) break;
+            if (k && bytes + need > c->arena) break;
             bytes += need;
             ++k;
             ++i;
