@@ -139,6 +139,13 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
     lvlip_launch_cfg cfg{};
     cfg.kernel = LVLIP_KERNEL_AUTO;  // the piece's average length picks the kernel
     cfg.len_hint = (int32_t)(bytes / count > 0x7fffffffull ? 0x7fffffff : bytes / count);
+    if (dev_base && cfg.len_hint >= 896) {
+        // packets read in place over PCIe: the flat sweep (U 8) reads them
+        // faster than the stream kernel AUTO picks from 896 B for HBM
+        // (scripts/lab_zerocopy.py)
+        cfg.kernel = LVLIP_KERNEL_FLAT;
+        cfg.unroll = 8;
+    }
     if (bytes <= c->direct_max && (dev_base || !src || src == s.h_bytes)) {
         // A small piece: the copies' fixed costs (an SDMA round trip each way)
         // outweigh moving the bytes, so the kernel reads the pinned arena (or
