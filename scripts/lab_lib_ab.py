@@ -12,7 +12,8 @@ box with the tree):
     python scripts/lab_lib_ab.py OUT.json [WORKLOAD] [ROUNDS]
     python scripts/lab_lib_ab.py OUT.json frames [ROUNDS]   # the host frame calls
 
-LAB_ARENA sets the contexts' arena bytes (default 256 MiB, as bench.py --e2e).
+LAB_ARENA sets the contexts' arena bytes (default 256 MiB, as bench.py --e2e);
+LAB_FRAME_SRC the frame calls' sources (default slab,dma; also zerocopy).
 
 Both libraries are driven through their C ABI only (ctypes); every call's
 outputs are compared with the first call's.
@@ -70,11 +71,12 @@ def frames_ab(path, libs, rounds, arena, reps=3):
     res = {"frames": n, "arena": arena, "GBps": {}}
     for _ in range(rounds):
         for name, lib in libs.items():
-            for src in ("slab", "dma"):
+            for src in os.environ.get("LAB_FRAME_SRC", "slab,dma").split(","):
                 h = ctypes.c_void_p()
                 assert lib.lvlip_csum_ctx_create(ctypes.byref(h), 0, arena) == 0
-                if src == "dma":
-                    assert lib.lvlip_csum_register(h, host.ctypes.data, host.size, lvlip.REG_DMA) == 0
+                if src in ("dma", "zerocopy"):
+                    flag = lvlip.REG_DMA if src == "dma" else lvlip.REG_ZEROCOPY
+                    assert lib.lvlip_csum_register(h, host.ctypes.data, host.size, flag) == 0
                 for call, fn in (("tx", lambda: lib.lvlip_tx_checksum(h, fr.ctypes.data, n)),
                                  ("rx_l4", lambda: lib.lvlip_rx_verify(h, fr.ctypes.data, n, lvlip.RX_VERIFY_L4,
                                                                        verdict.ctypes.data))):
