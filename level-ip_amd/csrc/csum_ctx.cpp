@@ -72,22 +72,22 @@ int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes, uint6
 // Two slots' copies issued on their own streams run side by side, share the
 // link and finish together; each slot's kernel and result copy then ran with
 // the link idle, 8.5 % of a registered batch's time (the pipeline's trace,
-// DESIGN.md §5).  On one copy stream the copies run back to back in issue
-// order, and each piece is summed and its results come back while the next
-// piece's copy runs.
+// DESIGN.md §5).  Each piece's copy now waits for the previous piece's (the
+// other slot's) copy event, so the copies run one after the other in issue
+// order and each piece is summed while the next one's copy runs.  The first
+// piece of a call waits for nothing: a cross-stream wait in front of a
+// call's only piece cost small batches up to ~0.5 ms (a copy stream shared
+// by both slots, tried first, did that for every piece).
 int h2d_ordered(lvlip_csum_ctx* c, Slot& s, void* dst, const void* src, size_t n, const char* what) {
     hipError_t e;
-    if (!c->copy_order) {
-        if ((e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s.stream)) != hipSuccess)
-            return fail(c, e, what);
-        return LVLIP_OK;
+    if (c->copy_order && c->last_copy && c->last_copy != &s &&
+        (e = hipStreamWaitEvent(s.stream, c->last_copy->copied, 0)) != hipSuccess)
+        return fail(c, e, "hipStreamWaitEvent");
+    if ((e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s.stream)) != hipSuccess) return fail(c, e, what);
+    if (c->copy_order) {
+        if ((e = hipEventRecord(s.copied, s.stream)) != hipSuccess) return fail(c, e, "hipEventRecord");
+        c->last_copy = &s;
     }
-    // the slot's previous piece is drained (its kernel done) before the slot
-    // takes a new one, so the copy needs no wait of its own
-    if ((e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->copy_stream)) != hipSuccess)
-        return fail(c, e, what);
-    if ((e = hipEventRecord(s.copied, c->copy_stream)) != hipSuccess) return fail(c, e, "hipEventRecord");
-    if ((e = hipStreamWaitEvent(s.stream, s.copied, 0)) != hipSuccess) return fail(c, e, "hipStreamWaitEvent");
     return LVLIP_OK;
 }
 
@@ -96,10 +96,9 @@ int finish_pieces(lvlip_csum_ctx* c, int rc) {
         const int r2 = drain(c, s);
         if (rc == LVLIP_OK) rc = r2;
     }
-    if (rc != LVLIP_OK) {
+    if (rc != LVLIP_OK)
         for (auto& s : c->slot) (void)hipStreamSynchronize(s.stream);
-        if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
-    }
+    c->last_copy = nullptr;  // the next call's first piece waits for nothing
     return rc;
 }
 
@@ -330,12 +329,6 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
             return LVLIP_ENOMEM;
         }
     }
-    if (const hipError_t e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking); e != hipSuccess) {
-        fail(c, e, "lvlip_csum_ctx_create");
-        for (auto& t : c->slot) free_slot(t);
-        delete c;
-        return LVLIP_ENOMEM;
-    }
     *out = c;
     return LVLIP_OK;
 }
@@ -343,12 +336,10 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
 int lvlip_csum_ctx_destroy(lvlip_csum_ctx* c) {
     if (!c) return LVLIP_EINVAL;
     DeviceGuard g(c->device);
-    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     for (auto& s : c->slot) {
         if (s.busy) (void)hipEventSynchronize(s.done);
         free_slot(s);
     }
-    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     for (const Region& r : c->regions) (void)hipHostUnregister(r.host);
     free(c->frame_scratch);
     free(c->frame_scratch2);

@@ -77,10 +77,11 @@ struct lvlip_csum_ctx {
     uint64_t piece = 0;       // bytes per piece (<= arena; a larger packet gets its own)
     uint64_t first_piece = 0; // frame calls: the first piece's bytes (doubling up to `piece`)
     uint64_t block_min = 0;   // pieces of at least this many bytes are waited for asleep (0: never)
-    // LVLIP_COPY_ORDER (default 1): every piece's H2D of its bytes goes on the
-    // one copy stream, in issue order (h2d_ordered); 0: on the slot's stream
+    // LVLIP_COPY_ORDER (default 1): each piece's H2D of its bytes waits for
+    // the previous piece's of the same call (h2d_ordered); last_copy is the
+    // slot that issued that one (nullptr at a call's start)
     int copy_order = 1;
-    hipStream_t copy_stream = nullptr;
+    lvlip_ctx::Slot* last_copy = nullptr;
     // frame calls' per-call host arrays (TX records and undo values, RX + L4
     // lengths), kept across calls: fresh pages would fault on every call
     void* frame_scratch = nullptr;
@@ -98,14 +99,13 @@ namespace lvlip_ctx {
 
 // Records a HIP failure in the context (and on stderr); returns `code`.
 int fail(lvlip_csum_ctx* c, hipError_t e, const char* what, int code = LVLIP_EHIP);
-// H2D of a piece's bytes into the slot: on the context's copy stream behind
-// the previous piece's, the slot's stream waiting for it (c->copy_order), or
-// on the slot's stream.
+// H2D of a piece's bytes into the slot, on the slot's stream, queued behind
+// the previous piece's copy of the same call when c->copy_order is set.
 int h2d_ordered(lvlip_csum_ctx* c, Slot& s, void* dst, const void* src, size_t n, const char* what);
 // Waits for a slot's in-flight piece and copies its results to user_out.
 int drain(lvlip_csum_ctx* c, Slot& s);
 // End of a batch call: drains both slots; after a failure also waits for what
-// a half-enqueued piece left on the slot streams and the copy stream.
+// a half-enqueued piece left on the slot streams.
 int finish_pieces(lvlip_csum_ctx* c, int rc);
 // The registered region holding [p, p + len), or nullptr.
 const Region* find_region(const lvlip_csum_ctx* c, const void* p, uint64_t len);

@@ -152,10 +152,9 @@ struct FrameSlots {
             const int r2 = drain_slot((next + j) % kSlots);
             if (rc == LVLIP_OK) rc = r2;
         }
-        if (rc != LVLIP_OK) {
+        if (rc != LVLIP_OK)
             for (auto& s : c->slot) (void)hipStreamSynchronize(s.stream);
-            if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
-        }
+        c->last_copy = nullptr;  // the next call's first piece waits for nothing
         return rc;
     }
 };

@@ -11,6 +11,7 @@ box with the tree):
     mkdir -p level-ip_amd/build/prev && cp /tmp/prev/level-ip_amd/liblvlip_csum.so level-ip_amd/build/prev/
     python scripts/lab_lib_ab.py OUT.json [WORKLOAD] [ROUNDS]
     python scripts/lab_lib_ab.py OUT.json frames [ROUNDS]   # the host frame calls
+    python scripts/lab_lib_ab.py OUT.json latency [ROUNDS]  # small host batches (64 MiB arena)
 
 LAB_ARENA sets the contexts' arena bytes (default 256 MiB, as bench.py --e2e);
 LAB_FRAME_SRC the frame calls' sources (default slab,dma; also zerocopy).
@@ -95,6 +96,40 @@ def frames_ab(path, libs, rounds, arena, reps=3):
         json.dump(res, f, indent=1)
 
 
+def latency_ab(path, libs, rounds, arena):
+    """Small host batches (n x 1500 B from plain memory, lvlip_csum_batch_host_flat):
+    the mean wall time of 100 synchronised calls per library, as bench.py
+    --e2e's diag.latency_us times them."""
+    import lvlip
+    import workloads
+
+    res = {"arena": arena, "us": {}}
+    bs = {n: workloads.make("tcp1500", n=n) for n in (64, 1024, 16384)}
+    for _ in range(rounds):
+        for name, lib in libs.items():
+            h = ctypes.c_void_p()
+            assert lib.lvlip_csum_ctx_create(ctypes.byref(h), 0, arena) == 0
+            for n, b in bs.items():
+                host = np.ascontiguousarray(b.host_bytes())
+                d = np.ascontiguousarray(b.descs, dtype=lvlip.DESC_DTYPE)
+                out = np.empty(b.n, np.uint16)
+
+                def call():
+                    assert lib.lvlip_csum_batch_host_flat(h, host.ctypes.data, host.size, d.ctypes.data, b.n,
+                                                          out.ctypes.data) == 0
+                for _ in range(20):
+                    call()
+                t0 = time.perf_counter()
+                for _ in range(100):
+                    call()
+                key = f"{name} n{n}"
+                res["us"].setdefault(key, []).append(round((time.perf_counter() - t0) / 100 * 1e6, 1))
+                print(key, res["us"][key], flush=True)
+            lib.lvlip_csum_ctx_destroy(h)
+    with open(path, "w") as f:
+        json.dump(res, f, indent=1)
+
+
 def main(path, workload="tcp1500", rounds=3, reps=3):
     import lvlip
     import workloads
@@ -104,6 +139,8 @@ def main(path, workload="tcp1500", rounds=3, reps=3):
     arena = int(os.environ.get("LAB_ARENA", 256 << 20))
     if workload == "frames":
         return frames_ab(path, libs, rounds, arena)
+    if workload == "latency":
+        return latency_ab(path, libs, rounds, int(os.environ.get("LAB_ARENA", 64 << 20)))
     b = workloads.make(workload)
     host = np.ascontiguousarray(b.host_bytes())
     d = np.ascontiguousarray(b.descs, dtype=lvlip.DESC_DTYPE)
