@@ -643,9 +643,9 @@ def test_host_direct_and_copied_pieces(monkeypatch, direct_max):
 
 @pytest.mark.parametrize("copy_order", ["0", "1"])
 def test_host_copy_order(monkeypatch, copy_order):
-    """LVLIP_COPY_ORDER (read when a context is made): 1 (the default) puts
-    every piece's H2D of its bytes on the context's one copy stream, the slot's
-    stream waiting for it; 0 issues it on the slot's stream.  Many small pieces
+    """LVLIP_COPY_ORDER (read when a context is made): 1 (the default) has
+    every piece's H2D of its bytes wait for the previous piece's copy of the
+    same call (the other slot's stream); 0 does not.  Many small pieces
     (a 256 KiB arena, no direct pieces) from the gather, a DMA region and the
     iov path, and the frame calls from a DMA region: the same bits either way."""
     monkeypatch.setenv("LVLIP_COPY_ORDER", copy_order)
