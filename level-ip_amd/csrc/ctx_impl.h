@@ -77,9 +77,10 @@ struct lvlip_csum_ctx {
     uint64_t piece = 0;       // bytes per piece (<= arena; a larger packet gets its own)
     uint64_t first_piece = 0; // frame calls: the first piece's bytes (doubling up to `piece`)
     uint64_t block_min = 0;   // pieces of at least this many bytes are waited for asleep (0: never)
-    // LVLIP_COPY_ORDER (default 1): each piece's H2D of its bytes waits for
-    // the previous piece's of the same call (h2d_ordered); last_copy is the
-    // slot that issued that one (nullptr at a call's start)
+    // LVLIP_COPY_ORDER (default 1): in the packet batch calls each piece's
+    // H2D of its bytes waits for the previous piece's of the same call
+    // (h2d_ordered; the frame calls do not); last_copy is the slot that
+    // issued that one (nullptr at a call's start)
     int copy_order = 1;
     lvlip_ctx::Slot* last_copy = nullptr;
     // frame calls' per-call host arrays (TX records and undo values, RX + L4

@@ -14,7 +14,10 @@ box with the tree):
     python scripts/lab_lib_ab.py OUT.json latency [ROUNDS]  # small host batches (64 MiB arena)
 
 LAB_ARENA sets the contexts' arena bytes (default 256 MiB, as bench.py --e2e);
-LAB_FRAME_SRC the frame calls' sources (default slab,dma; also zerocopy).
+LAB_FRAME_SRC the frame calls' sources (default slab,dma; also zerocopy);
+LAB_PREV_LIB=cur makes "prev" this tree's library too, and LAB_ENV_CUR /
+LAB_ENV_PREV ("K=V,K=V") set knobs for each side's contexts: an env A/B of
+one build in one process.
 
 Both libraries are driven through their C ABI only (ctypes); every call's
 outputs are compared with the first call's.
@@ -45,6 +48,25 @@ def bind(path):
     return lib
 
 
+def ctx_create(name, lib, arena):
+    """lvlip_csum_ctx_create under the environment LAB_ENV_<NAME> ("K=V,K=V";
+    the context reads its knobs when it is made)."""
+    env = os.environ.get(f"LAB_ENV_{name.upper()}", "")
+    kv = [e.split("=", 1) for e in env.split(",") if e]
+    old = {k: os.environ.get(k) for k, _ in kv}
+    os.environ.update(dict(kv))
+    try:
+        h = ctypes.c_void_p()
+        assert lib.lvlip_csum_ctx_create(ctypes.byref(h), 0, arena) == 0
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return h
+
+
 def frames_ab(path, libs, rounds, arena, reps=3):
     """The host frame calls (TX fill, RX + L4) on 512K of bench.py's mixed
     frames in host memory, from a plain slab and from the slab registered
@@ -73,8 +95,7 @@ def frames_ab(path, libs, rounds, arena, reps=3):
     for _ in range(rounds):
         for name, lib in libs.items():
             for src in os.environ.get("LAB_FRAME_SRC", "slab,dma").split(","):
-                h = ctypes.c_void_p()
-                assert lib.lvlip_csum_ctx_create(ctypes.byref(h), 0, arena) == 0
+                h = ctx_create(name, lib, arena)
                 if src in ("dma", "zerocopy"):
                     flag = lvlip.REG_DMA if src == "dma" else lvlip.REG_ZEROCOPY
                     assert lib.lvlip_csum_register(h, host.ctypes.data, host.size, flag) == 0
@@ -83,13 +104,16 @@ def frames_ab(path, libs, rounds, arena, reps=3):
                                                                        verdict.ctypes.data))):
                     assert fn() == 0
                     best = 0.0
+                    c0 = time.process_time()
                     for _ in range(reps):
                         t0 = time.perf_counter()
                         assert fn() == 0
                         best = max(best, hb / (time.perf_counter() - t0) / 1e9)
+                    cpu_ns = (time.process_time() - c0) / reps / n * 1e9
                     key = f"{name} {src} {call}"
                     res["GBps"].setdefault(key, []).append(round(best, 2))
-                    print(key, res["GBps"][key], flush=True)
+                    res.setdefault("cpu_ns_per_frame", {}).setdefault(key, []).append(round(cpu_ns, 1))
+                    print(key, res["GBps"][key], res["cpu_ns_per_frame"][key], flush=True)
                 assert np.array_equal(host, want), (name, src)  # the TX fill is idempotent
                 lib.lvlip_csum_ctx_destroy(h)
     with open(path, "w") as f:
@@ -107,8 +131,7 @@ def latency_ab(path, libs, rounds, arena):
     bs = {n: workloads.make("tcp1500", n=n) for n in (64, 1024, 16384)}
     for _ in range(rounds):
         for name, lib in libs.items():
-            h = ctypes.c_void_p()
-            assert lib.lvlip_csum_ctx_create(ctypes.byref(h), 0, arena) == 0
+            h = ctx_create(name, lib, arena)
             for n, b in bs.items():
                 host = np.ascontiguousarray(b.host_bytes())
                 d = np.ascontiguousarray(b.descs, dtype=lvlip.DESC_DTYPE)
@@ -134,8 +157,8 @@ def main(path, workload="tcp1500", rounds=3, reps=3):
     import lvlip
     import workloads
 
-    libs = {"cur": bind(lvlip.LIB_PATH),
-            "prev": bind(os.path.join(ROOT, "level-ip_amd", "build", "prev", "liblvlip_csum.so"))}
+    prev = os.environ.get("LAB_PREV_LIB", os.path.join(ROOT, "level-ip_amd", "build", "prev", "liblvlip_csum.so"))
+    libs = {"cur": bind(lvlip.LIB_PATH), "prev": bind(lvlip.LIB_PATH if prev == "cur" else prev)}
     arena = int(os.environ.get("LAB_ARENA", 256 << 20))
     if workload == "frames":
         return frames_ab(path, libs, rounds, arena)
@@ -154,8 +177,7 @@ def main(path, workload="tcp1500", rounds=3, reps=3):
     for _ in range(rounds):
         for name, lib in libs.items():
             for src in ("gather", "dma", "zerocopy", "iov"):
-                h = ctypes.c_void_p()
-                assert lib.lvlip_csum_ctx_create(ctypes.byref(h), 0, arena) == 0
+                h = ctx_create(name, lib, arena)
                 if src in ("dma", "zerocopy"):
                     flag = lvlip.REG_DMA if src == "dma" else lvlip.REG_ZEROCOPY
                     assert lib.lvlip_csum_register(h, host.ctypes.data, host.size, flag) == 0
