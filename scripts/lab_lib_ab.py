@@ -14,7 +14,7 @@ box with the tree):
     python scripts/lab_lib_ab.py OUT.json latency [ROUNDS]  # small host batches (64 MiB arena)
 
 LAB_ARENA sets the contexts' arena bytes (default 256 MiB, as bench.py --e2e);
-LAB_FRAME_SRC the frame calls' sources (default slab,dma; also zerocopy);
+LAB_FRAME_SRC the frame calls' sources (default slab,dma; also zerocopy, scattered);
 LAB_PREV_LIB=cur makes "prev" this tree's library too, and LAB_ENV_CUR /
 LAB_ENV_PREV ("K=V,K=V") set knobs for each side's contexts: an env A/B of
 one build in one process.
@@ -88,6 +88,16 @@ def frames_ab(path, libs, rounds, arena, reps=3):
     fr = np.zeros(n, dtype=[("head", "<u8"), ("len", "<u4"), ("pad", "<u4")])
     fr["head"] = host.ctypes.data + fd["offset"][:n].astype(np.uint64)
     fr["len"] = fd["len"][:n]
+    # the same frames scattered: each at the start of its own 1616-B slot, the
+    # slots in random order (bench.py --frames' scattered source)
+    stride = 1616
+    slot = np.random.default_rng(7).permutation(n)
+    scat = np.zeros(n * stride, np.uint8)
+    for i in range(n):
+        o, ln = int(fd["offset"][i]), int(fd["len"][i])
+        scat[int(slot[i]) * stride:int(slot[i]) * stride + ln] = host[o:o + ln]
+    frs = fr.copy()
+    frs["head"] = scat.ctypes.data + slot.astype(np.uint64) * stride
     hb = 20 * n + int(pay["len"][:n].sum())
     verdict = np.zeros(n, np.uint8)
     want = host.copy()
@@ -99,8 +109,9 @@ def frames_ab(path, libs, rounds, arena, reps=3):
                 if src in ("dma", "zerocopy"):
                     flag = lvlip.REG_DMA if src == "dma" else lvlip.REG_ZEROCOPY
                     assert lib.lvlip_csum_register(h, host.ctypes.data, host.size, flag) == 0
-                for call, fn in (("tx", lambda: lib.lvlip_tx_checksum(h, fr.ctypes.data, n)),
-                                 ("rx_l4", lambda: lib.lvlip_rx_verify(h, fr.ctypes.data, n, lvlip.RX_VERIFY_L4,
+                arr = frs if src == "scattered" else fr
+                for call, fn in (("tx", lambda: lib.lvlip_tx_checksum(h, arr.ctypes.data, n)),
+                                 ("rx_l4", lambda: lib.lvlip_rx_verify(h, arr.ctypes.data, n, lvlip.RX_VERIFY_L4,
                                                                        verdict.ctypes.data))):
                     assert fn() == 0
                     best = 0.0
