@@ -753,6 +753,27 @@ def test_host_registered_regions(flags):
         ctx.register(buf, flags)  # left registered: destroy releases it
 
 
+@pytest.mark.parametrize("flags", [lvlip.REG_DMA, lvlip.REG_ZEROCOPY])
+@pytest.mark.parametrize("name,n", [("tcp1500", 4000), ("tcp9000", 700)])
+def test_host_registered_regions_long_packets(flags, name, n):
+    """Registered regions with MTU and jumbo packets: pieces span the arena
+    (several here), and zero-copy pieces of >= 896-B packets run the flat
+    sweep over PCIe instead of AUTO's stream kernel (csum_ctx.cpp
+    launch_piece); the same bits as the oracle either way."""
+    b = workloads.make(name, n=n)
+    host = np.empty(b.nbytes + 4096 + 5, dtype=np.uint8)
+    buf = host[5:5 + b.nbytes]
+    buf[:] = b.host_bytes()
+    want = pyoracle.batch(buf, b.descs, threads=THREADS)
+    with lvlip.Context(0, arena_bytes=1 << 20) as ctx:
+        ctx.register(buf, flags)
+        assert np.array_equal(ctx.batch_host_flat(buf, b.descs), want)
+        pk = [buf[int(d["offset"]):int(d["offset"]) + int(d["len"])] for d in b.descs]
+        st = [int(d["start_sum"]) for d in b.descs]
+        assert np.array_equal(ctx.batch_host(pk, st), want)
+        ctx.unregister(buf)
+
+
 def test_contexts_in_threads():
     """One context per thread (the reference checksums from the core, IPC and
     timer threads, src/main.c:83-89): concurrent host batches stay bit-exact."""
