@@ -185,7 +185,7 @@ static void frame_calls(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed) {
 // registered in `reg` mode (DMA: the copy engine reads spans; ZEROCOPY: the
 // kernel reads in place), and as received skbs: BUFLEN-long buffers holding
 // shorter frames (src/netdev.c:89-91), unregistered.
-static void frame_slab(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed, int reg) {
+static void frame_slab(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed, int reg, uint32_t gap = 24) {
     Rng r{seed};
     std::vector<uint32_t> len(n), off(n);
     std::vector<bool> tcp(n);
@@ -195,7 +195,7 @@ static void frame_slab(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed, int reg) 
         bool t;
         len[i] = frame_len(r, t, ihl[i], l4h[i]);
         tcp[i] = t;
-        pos += r() % 24u;
+        pos += r() % gap;
         off[i] = (uint32_t)pos;
         pos += len[i];
     }
@@ -244,6 +244,9 @@ int main() {
     frame_slab(ctx, 20000, 7, -1);
     frame_slab(ctx, 20000, 8, (int)LVLIP_REG_DMA);
     frame_slab(ctx, 5000, 9, (int)LVLIP_REG_ZEROCOPY);
+    // frames spread thinly over a zero-copy region (gaps of up to 8 KiB): read
+    // in place rather than moved as spans
+    frame_slab(ctx, 3000, 10, (int)LVLIP_REG_ZEROCOPY, 8192);
 
     // a packet larger than the arena is refused; nothing is read
     std::vector<uint8_t> big((2u << 20) + 5u, 0xab);

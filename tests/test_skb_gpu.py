@@ -131,10 +131,12 @@ def test_empty(ctx):
 #
 # The host frame calls parse on the device (frames_host.cpp): scattered frames
 # are gathered whole into the pinned arena, frames in a registered region are
-# DMA'd as spans (LVLIP_REG_DMA) or read in place (LVLIP_REG_ZEROCOPY).  The
-# same frames through every source must give the oracle's verdicts and fill.
+# DMA'd as spans (LVLIP_REG_DMA, and LVLIP_REG_ZEROCOPY when the frames lie
+# densely in it) or read in place (LVLIP_REG_ZEROCOPY, frames spread thinly
+# over the region: "zerocopy_sparse", one frame per 4 KiB).  The same frames
+# through every source must give the oracle's verdicts and fill.
 
-SOURCES = ("scattered", "slab", "dma", "zerocopy")
+SOURCES = ("scattered", "slab", "dma", "zerocopy", "zerocopy_sparse")
 
 
 def _frames_in(source, frames, seed):
@@ -143,18 +145,33 @@ def _frames_in(source, frames, seed):
     order), unregistered or to be registered."""
     if source == "scattered":
         return [bytearray(f) for f in frames], None
+    if source == "zerocopy_sparse":
+        # one frame per 4 KiB (jumbo frames take more), at a random offset mod
+        # 16: the region's span is well over twice the frames' bytes
+        rng = np.random.default_rng(seed)
+        offs, pos = [], 0
+        for f in frames:
+            o = pos + int(rng.integers(0, 16))
+            offs.append(o)
+            pos = (o + len(f) + 4095) // 4096 * 4096
+        buf = np.zeros(pos + 64, dtype=np.uint8)
+        views = []
+        for o, f in zip(offs, frames):
+            buf[o:o + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
+            views.append(buf[o:o + len(f)])
+        return views, buf
     buf, fd = lvlip.pack_frames(frames, align_mod=16, seed=seed)
     views = [buf[int(d["offset"]):int(d["offset"]) + int(d["len"])] for d in fd]
     return views, buf
 
 
 def _registered(ctx, source, buf):
-    if source in ("dma", "zerocopy"):
+    if source in ("dma", "zerocopy", "zerocopy_sparse"):
         ctx.register(buf, lvlip.REG_DMA if source == "dma" else lvlip.REG_ZEROCOPY)
 
 
 def _unregister(ctx, source, buf):
-    if source in ("dma", "zerocopy"):
+    if source in ("dma", "zerocopy", "zerocopy_sparse"):
         ctx.unregister(buf)
 
 
