@@ -229,7 +229,11 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx *ctx, const void *base,
  *   LVLIP_REG_ZEROCOPY  the kernel reads the packets in place over PCIe: only
  *                       descriptors go down and results come back, for
  *                       batch_host (any packets inside the region) and
- *                       batch_host_flat alike
+ *                       batch_host_flat alike.  The frame calls of
+ *                       lvlip_skb.h read frames spread thinly over the region
+ *                       in place too, and move frames that lie densely in it
+ *                       as spans with the copy engine, as for LVLIP_REG_DMA
+ *                       (their per-frame parse reads over PCIe cost ~15 %)
  * Regions must not overlap; the memory must stay valid until unregistered
  * (lvlip_csum_ctx_destroy unregisters what is left).  Results are identical
  * on every path. */
