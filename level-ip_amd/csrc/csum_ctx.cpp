@@ -195,6 +195,31 @@ int first_failure(lvlip_csum_ctx* c, uint32_t n, const F& check) {
     return f == ~0ull ? LVLIP_OK : -(int)(f & 0xffu);
 }
 
+// Whether a flat batch's packets cover their byte span densely (the span at
+// most twice their bytes plus 1 MiB, the frame calls' rule), on the pool
+// threads.
+bool dense_span(lvlip_csum_ctx* c, const lvlip_csum_desc* d, uint32_t n) {
+    std::atomic<uint64_t> lo{~0ull}, hi{0}, sum{0};
+    parallel_ranges(c, n, 65536, [&lo, &hi, &sum, d](uint64_t a, uint64_t z) {
+        uint64_t l = ~0ull, h = 0, t = 0;
+        for (uint64_t q = a; q < z; ++q) {
+            const uint64_t len = d[q].len > 0 ? (uint64_t)d[q].len : 0u, e = d[q].offset + len;
+            l = d[q].offset < l ? d[q].offset : l;
+            h = e > h ? e : h;
+            t += len;
+        }
+        uint64_t cur = lo.load(std::memory_order_relaxed);
+        while (l < cur && !lo.compare_exchange_weak(cur, l, std::memory_order_relaxed)) {
+        }
+        cur = hi.load(std::memory_order_relaxed);
+        while (h > cur && !hi.compare_exchange_weak(cur, h, std::memory_order_relaxed)) {
+        }
+        sum.fetch_add(t, std::memory_order_relaxed);
+    });
+    const uint64_t l = lo.load(), h = hi.load();
+    return h > l && h - l <= 2 * sum.load() + (1ull << 20);
+}
+
 // Zero-copy: descriptors only (offsets from the region's first byte rounded
 // down to 16), kernel reads the registered pages in place.  `offset_of(i)`
 // gives packet i's byte address; the whole batch lies in region `r`.  Pieces
@@ -487,7 +512,10 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
     if (bad != LVLIP_OK) return bad;
     DeviceGuard g(c->device);
     const Region* reg = c->regions.empty() ? nullptr : find_region(c, b, base_bytes);
-    if (reg && (reg->flags & LVLIP_REG_ZEROCOPY))
+    // a zero-copy region is read in place, unless the batch covers its span
+    // densely: then the copy engine moves the spans as from a DMA region
+    // (tcp1500: 54.6-55.2 against 52.5 GB/s in place)
+    if (reg && (reg->flags & LVLIP_REG_ZEROCOPY) && !dense_span(c, d, n))
         return zerocopy_batch(
             c, *reg, n, out, [&](uint32_t q) { return b + d[q].offset; },
             [&](uint32_t q) { return d[q]; }, [&](uint32_t q) { return d[q].len; });

@@ -74,12 +74,12 @@ static void scattered(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_
 
 // One flat buffer that ends at the last packet's last byte (not a multiple of
 // 16), packets at every alignment with gaps; optionally registered.
-static void flat(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_t seed, int reg) {
+static void flat(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_t seed, int reg, uint32_t gap = 40) {
     Rng r{seed};
     std::vector<lvlip_csum_desc> d(n);
     uint64_t off = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        off += r() % 40u;
+        off += r() % gap;
         d[i].offset = off;
         d[i].len = (int32_t)(r() % (max_len + 1));
         d[i].start_sum = r();
@@ -240,6 +240,9 @@ int main() {
     flat(ctx, 20000, 1600, 3, -1);
     flat(ctx, 20000, 1600, 4, (int)LVLIP_REG_DMA);
     flat(ctx, 5000, 1600, 5, (int)LVLIP_REG_ZEROCOPY);
+    // packets spread thinly over a zero-copy region: read in place (a dense
+    // batch moves as spans, as from a DMA region)
+    flat(ctx, 3000, 1600, 11, (int)LVLIP_REG_ZEROCOPY, 8192);
     frame_calls(ctx, 20000, 6);
     frame_slab(ctx, 20000, 7, -1);
     frame_slab(ctx, 20000, 8, (int)LVLIP_REG_DMA);

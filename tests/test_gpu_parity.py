@@ -774,6 +774,30 @@ def test_host_registered_regions_long_packets(flags, name, n):
         ctx.unregister(buf)
 
 
+@pytest.mark.parametrize("gap", [0, 6000])
+def test_host_zerocopy_flat_dense_and_sparse(gap):
+    """A flat batch over a LVLIP_REG_ZEROCOPY region: packets that cover their
+    span densely move as spans with the copy engine (as from a DMA region),
+    packets spread thinly (gap: bytes added between consecutive packets) are
+    read in place by the kernel; the oracle's bits either way."""
+    b = workloads.make("mixed", n=8000)
+    src = b.host_bytes()
+    d = np.array(b.descs, copy=True)
+    shift = np.arange(d.size, dtype=np.uint64) * np.uint64(gap)
+    d["offset"] = d["offset"] + shift
+    nbytes = int(d["offset"][-1]) + int(d["len"][-1]) + 64
+    host = np.zeros(nbytes + 4096, dtype=np.uint8)
+    buf = host[:nbytes]
+    for i in range(d.size):
+        o0, o1, ln = int(b.descs["offset"][i]), int(d["offset"][i]), max(int(d["len"][i]), 0)
+        buf[o1:o1 + ln] = src[o0:o0 + ln]
+    want = pyoracle.batch(buf, d, threads=THREADS)
+    with lvlip.Context(0, arena_bytes=1 << 20) as ctx:
+        ctx.register(buf, lvlip.REG_ZEROCOPY)
+        assert np.array_equal(ctx.batch_host_flat(buf, d), want)
+        ctx.unregister(buf)
+
+
 def test_contexts_in_threads():
     """One context per thread (the reference checksums from the core, IPC and
     timer threads, src/main.c:83-89): concurrent host batches stay bit-exact."""
