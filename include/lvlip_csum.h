@@ -225,16 +225,17 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx *ctx, const void *base,
  * one registered region skip the gather into the pinned arena:
  *   LVLIP_REG_DMA       batch_host_flat copies each piece's span straight
  *                       from the region with the copy engine (no CPU memcpy);
- *                       batch_host (scattered packets) still gathers
+ *                       so does batch_host when its packets cover their span
+ *                       densely (else it gathers them)
  *   LVLIP_REG_ZEROCOPY  the kernel reads the packets in place over PCIe: only
  *                       descriptors go down and results come back, for
- *                       batch_host (any packets inside the region) and for
- *                       batch_host_flat and the frame calls of lvlip_skb.h
- *                       when their packets / frames lie thinly over the
- *                       region; when they cover their span densely those two
- *                       move it with the copy engine, as for LVLIP_REG_DMA
- *                       (faster: 5 % for packet batches, ~20 % for the frame
- *                       calls, whose per-frame parse reads over PCIe)
+ *                       batch_host, batch_host_flat and the frame calls of
+ *                       lvlip_skb.h when their packets / frames lie thinly
+ *                       over the region; when they cover their span densely
+ *                       the span moves with the copy engine, as for
+ *                       LVLIP_REG_DMA (faster: 2-5 % for packet batches,
+ *                       ~20 % for the frame calls, whose per-frame parse reads
+ *                       over PCIe)
  * Regions must not overlap; the memory must stay valid until unregistered
  * (lvlip_csum_ctx_destroy unregisters what is left).  Results are identical
  * on every path. */

@@ -195,18 +195,21 @@ int first_failure(lvlip_csum_ctx* c, uint32_t n, const F& check) {
     return f == ~0ull ? LVLIP_OK : -(int)(f & 0xffu);
 }
 
-// Whether a flat batch's packets cover their byte span densely (the span at
-// most twice their bytes plus 1 MiB, the frame calls' rule), on the pool
-// threads.
-bool dense_span(lvlip_csum_ctx* c, const lvlip_csum_desc* d, uint32_t n) {
+// Whether n packets (start address off_of(q), length len_of(q)) cover their
+// byte span densely: the span at most twice their bytes plus 1 MiB, the frame
+// calls' rule; on the pool threads.
+template <class Off, class Len>
+bool dense_span(lvlip_csum_ctx* c, uint32_t n, const Off& off_of, const Len& len_of) {
     std::atomic<uint64_t> lo{~0ull}, hi{0}, sum{0};
-    parallel_ranges(c, n, 65536, [&lo, &hi, &sum, d](uint64_t a, uint64_t z) {
+    parallel_ranges(c, n, 65536, [&](uint64_t a, uint64_t z) {
         uint64_t l = ~0ull, h = 0, t = 0;
         for (uint64_t q = a; q < z; ++q) {
-            const uint64_t len = d[q].len > 0 ? (uint64_t)d[q].len : 0u, e = d[q].offset + len;
-            l = d[q].offset < l ? d[q].offset : l;
+            const int32_t sl = len_of((uint32_t)q);
+            if (sl <= 0) continue;
+            const uint64_t o = off_of((uint32_t)q), e = o + (uint64_t)sl;
+            l = o < l ? o : l;
             h = e > h ? e : h;
-            t += len;
+            t += (uint64_t)sl;
         }
         uint64_t cur = lo.load(std::memory_order_relaxed);
         while (l < cur && !lo.compare_exchange_weak(cur, l, std::memory_order_relaxed)) {
@@ -218,6 +221,17 @@ bool dense_span(lvlip_csum_ctx* c, const lvlip_csum_desc* d, uint32_t n) {
     });
     const uint64_t l = lo.load(), h = hi.load();
     return h > l && h - l <= 2 * sum.load() + (1ull << 20);
+}
+
+// The context's scratch array for the host batch calls, at least `bytes`
+// (kept across calls: fresh pages would fault on every call).
+void* host_scratch(lvlip_csum_ctx* c, size_t bytes) {
+    if (c->host_scratch_bytes < bytes) {
+        free(c->host_scratch);
+        c->host_scratch = malloc(bytes);
+        c->host_scratch_bytes = c->host_scratch ? bytes : 0;
+    }
+    return c->host_scratch;
 }
 
 // Zero-copy: descriptors only (offsets from the region's first byte rounded
@@ -368,6 +382,7 @@ int lvlip_csum_ctx_destroy(lvlip_csum_ctx* c) {
     for (const Region& r : c->regions) (void)hipHostUnregister(r.host);
     free(c->frame_scratch);
     free(c->frame_scratch2);
+    free(c->host_scratch);
     delete c;
     return LVLIP_OK;
 }
@@ -424,17 +439,41 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
         return LVLIP_EINVAL;
     DeviceGuard g(c->device);
     if (!c->regions.empty()) {
-        // f3: all packets inside one zero-copy region -> no gather at all (the
-        // region of the first non-empty packet; regions never overlap)
+        // f3: all packets inside one registered region (the region of the
+        // first non-empty packet; regions never overlap) -> no gather at all:
+        // packets that cover their span densely go as a flat batch over the
+        // region (the copy engine moves the spans); a zero-copy region's
+        // sparse packets are read in place; a DMA region's sparse ones are
+        // gathered below
         uint32_t i0 = 0;
         while (i0 < n && pkts[i0].len <= 0) ++i0;
         const Region* r = i0 < n ? find_region(c, pkts[i0].ptr, (uint64_t)pkts[i0].len) : nullptr;
-        if (r && (r->flags & LVLIP_REG_ZEROCOPY) &&
-            first_failure(c, n, [pkts, r](uint32_t q) {
-                const uint8_t* a = (const uint8_t*)pkts[q].ptr;
-                return pkts[q].len <= 0 || (a >= r->host && a + pkts[q].len <= r->host + r->bytes) ? LVLIP_OK
-                                                                                                  : LVLIP_EINVAL;
-            }) == LVLIP_OK)
+        const bool inside = r && first_failure(c, n, [pkts, r](uint32_t q) {
+                                const uint8_t* a = (const uint8_t*)pkts[q].ptr;
+                                return pkts[q].len <= 0 || (a >= r->host && a + pkts[q].len <= r->host + r->bytes)
+                                           ? LVLIP_OK
+                                           : LVLIP_EINVAL;
+                            }) == LVLIP_OK;
+        if (inside && dense_span(
+                          c, n, [pkts](uint32_t q) { return (uint64_t)(uintptr_t)pkts[q].ptr; },
+                          [pkts](uint32_t q) { return pkts[q].len; })) {
+            lvlip_csum_desc* fd = (lvlip_csum_desc*)host_scratch(c, sizeof(lvlip_csum_desc) * (size_t)n);
+            if (fd) {
+                const uint8_t* r0 = r->host;
+                parallel_ranges(c, n, 65536, [fd, pkts, r0](uint64_t a, uint64_t z) {
+                    for (uint64_t q = a; q < z; ++q) {
+                        fd[q].offset = pkts[q].len > 0 ? (uint64_t)((const uint8_t*)pkts[q].ptr - r0) : 0u;
+                        fd[q].len = pkts[q].len;
+                        fd[q].start_sum = pkts[q].start_sum;
+                    }
+                });
+                // refused only when one packet's 16-B span exceeds the arena
+                // (the flat call's rule): then the gather below takes it
+                const int frc = lvlip_csum_batch_host_flat(c, r0, r->bytes, fd, n, out);
+                if (frc != LVLIP_ERANGE) return frc;
+            }
+        }
+        if (inside && (r->flags & LVLIP_REG_ZEROCOPY))
             return zerocopy_batch(
                 c, *r, n, out,
                 [&](uint32_t q) { return pkts[q].len > 0 ? (const uint8_t*)pkts[q].ptr : r->host; },
@@ -515,7 +554,8 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
     // a zero-copy region is read in place, unless the batch covers its span
     // densely: then the copy engine moves the spans as from a DMA region
     // (tcp1500: 54.6-55.2 against 52.5 GB/s in place)
-    if (reg && (reg->flags & LVLIP_REG_ZEROCOPY) && !dense_span(c, d, n))
+    if (reg && (reg->flags & LVLIP_REG_ZEROCOPY) &&
+        !dense_span(c, n, [d](uint32_t q) { return d[q].offset; }, [d](uint32_t q) { return d[q].len; }))
         return zerocopy_batch(
             c, *reg, n, out, [&](uint32_t q) { return b + d[q].offset; },
             [&](uint32_t q) { return d[q]; }, [&](uint32_t q) { return d[q].len; });

@@ -89,6 +89,9 @@ struct lvlip_csum_ctx {
     size_t frame_scratch_bytes = 0;
     void* frame_scratch2 = nullptr;
     size_t frame_scratch2_bytes = 0;
+    // the iov call's flat descriptors over a registered region, kept likewise
+    void* host_scratch = nullptr;
+    size_t host_scratch_bytes = 0;
     int frame_trace = 0;      // LVLIP_FRAME_TRACE=1: per-step host times on stderr
     lvlip_ctx::Slot slot[lvlip_ctx::kSlots];
     std::vector<lvlip_ctx::Region> regions;

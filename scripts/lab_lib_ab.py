@@ -15,6 +15,8 @@ box with the tree):
 
 LAB_ARENA sets the contexts' arena bytes (default 256 MiB, as bench.py --e2e);
 LAB_FRAME_SRC the frame calls' sources (default slab,dma; also zerocopy, scattered);
+LAB_SRC the packet batches' sources (default gather,dma,zerocopy,iov; also
+iov_dma, iov_zc: the iov call over the buffer registered);
 LAB_PREV_LIB=cur makes "prev" this tree's library too, and LAB_ENV_CUR /
 LAB_ENV_PREV ("K=V,K=V") set knobs for each side's contexts: an env A/B of
 one build in one process.
@@ -187,12 +189,12 @@ def main(path, workload="tcp1500", rounds=3, reps=3):
     res = {"workload": workload, "arena": arena, "GBps": {}}
     for _ in range(rounds):
         for name, lib in libs.items():
-            for src in ("gather", "dma", "zerocopy", "iov"):
+            for src in os.environ.get("LAB_SRC", "gather,dma,zerocopy,iov").split(","):
                 h = ctx_create(name, lib, arena)
-                if src in ("dma", "zerocopy"):
-                    flag = lvlip.REG_DMA if src == "dma" else lvlip.REG_ZEROCOPY
+                if src in ("dma", "zerocopy", "iov_dma", "iov_zc"):
+                    flag = lvlip.REG_DMA if src in ("dma", "iov_dma") else lvlip.REG_ZEROCOPY
                     assert lib.lvlip_csum_register(h, host.ctypes.data, host.size, flag) == 0
-                if src == "iov":
+                if src.startswith("iov"):
                     def call():
                         return lib.lvlip_csum_batch_host(h, iov.ctypes.data, b.n, out.ctypes.data)
                 else:
