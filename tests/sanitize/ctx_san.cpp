@@ -96,7 +96,8 @@ static void flat(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_t see
     for (uint32_t i = 0; i < n; ++i)
         CHECK(out[i] == oracle_checksum(base + d[i].offset, d[i].len, (int)d[i].start_sum),
               "flat %u reg %d", i, reg);
-    if (reg == (int)LVLIP_REG_ZEROCOPY) {  // scattered packets inside the region: in place
+    if (reg >= 0) {  // the same packets as an iov array inside the region: a flat
+                     // batch over it when dense, else in place (zero-copy) or gathered (DMA)
         std::vector<lvlip_csum_iov> iov(n);
         for (uint32_t i = 0; i < n; ++i) iov[i] = {base + d[i].offset, d[i].len, d[i].start_sum};
         std::fill(out.begin(), out.end(), 0);
