@@ -448,30 +448,51 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
         uint32_t i0 = 0;
         while (i0 < n && pkts[i0].len <= 0) ++i0;
         const Region* r = i0 < n ? find_region(c, pkts[i0].ptr, (uint64_t)pkts[i0].len) : nullptr;
-        const bool inside = r && first_failure(c, n, [pkts, r](uint32_t q) {
-                                const uint8_t* a = (const uint8_t*)pkts[q].ptr;
-                                return pkts[q].len <= 0 || (a >= r->host && a + pkts[q].len <= r->host + r->bytes)
-                                           ? LVLIP_OK
-                                           : LVLIP_EINVAL;
-                            }) == LVLIP_OK;
-        if (inside && dense_span(
-                          c, n, [pkts](uint32_t q) { return (uint64_t)(uintptr_t)pkts[q].ptr; },
-                          [pkts](uint32_t q) { return pkts[q].len; })) {
-            lvlip_csum_desc* fd = (lvlip_csum_desc*)host_scratch(c, sizeof(lvlip_csum_desc) * (size_t)n);
-            if (fd) {
-                const uint8_t* r0 = r->host;
-                parallel_ranges(c, n, 65536, [fd, pkts, r0](uint64_t a, uint64_t z) {
-                    for (uint64_t q = a; q < z; ++q) {
-                        fd[q].offset = pkts[q].len > 0 ? (uint64_t)((const uint8_t*)pkts[q].ptr - r0) : 0u;
-                        fd[q].len = pkts[q].len;
-                        fd[q].start_sum = pkts[q].start_sum;
+        // one pass on the pool threads: every packet inside r, the packets'
+        // span and bytes (dense?), and their flat descriptors relative to r
+        // (written whether or not they are used)
+        bool inside = false, dense = false;
+        lvlip_csum_desc* fd = nullptr;
+        if (r) {
+            fd = (lvlip_csum_desc*)host_scratch(c, sizeof(lvlip_csum_desc) * (size_t)n);
+            const uint8_t *r0 = r->host, *r1 = r->host + r->bytes;
+            std::atomic<bool> outside{false};
+            std::atomic<uint64_t> lo{~0ull}, hi{0}, sum{0};
+            parallel_ranges(c, n, 65536, [&, fd, r0, r1](uint64_t a, uint64_t z) {
+                uint64_t l = ~0ull, h = 0, t = 0;
+                for (uint64_t q = a; q < z; ++q) {
+                    const int32_t len = pkts[q].len;
+                    uint64_t o = 0;
+                    if (len > 0) {
+                        const uint8_t* p = (const uint8_t*)pkts[q].ptr;
+                        if (p < r0 || p + len > r1) {
+                            outside.store(true, std::memory_order_relaxed);
+                            return;
+                        }
+                        o = (uint64_t)(p - r0);
+                        l = o < l ? o : l;
+                        h = o + (uint64_t)len > h ? o + (uint64_t)len : h;
+                        t += (uint64_t)len;
                     }
-                });
-                // refused only when one packet's 16-B span exceeds the arena
-                // (the flat call's rule): then the gather below takes it
-                const int frc = lvlip_csum_batch_host_flat(c, r0, r->bytes, fd, n, out);
-                if (frc != LVLIP_ERANGE) return frc;
-            }
+                    if (fd) fd[q] = lvlip_csum_desc{o, len, pkts[q].start_sum};
+                }
+                uint64_t cur = lo.load(std::memory_order_relaxed);
+                while (l < cur && !lo.compare_exchange_weak(cur, l, std::memory_order_relaxed)) {
+                }
+                cur = hi.load(std::memory_order_relaxed);
+                while (h > cur && !hi.compare_exchange_weak(cur, h, std::memory_order_relaxed)) {
+                }
+                sum.fetch_add(t, std::memory_order_relaxed);
+            });
+            inside = !outside.load();
+            const uint64_t l = lo.load(), h = hi.load();
+            dense = inside && h > l && h - l <= 2 * sum.load() + (1ull << 20);
+        }
+        if (dense && fd) {
+            // refused only when one packet's 16-B span exceeds the arena (the
+            // flat call's rule): then the gather below takes it
+            const int frc = lvlip_csum_batch_host_flat(c, r->host, r->bytes, fd, n, out);
+            if (frc != LVLIP_ERANGE) return frc;
         }
         if (inside && (r->flags & LVLIP_REG_ZEROCOPY))
             return zerocopy_batch(
