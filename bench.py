@@ -94,6 +94,9 @@ def parse(argv=None):
     p.add_argument("--origin", choices=["local", "root"], default="local",
                    help="root: the whole batch starts on rank 0's GPU and is scattered "
                         "point to point first (timed separately, diag.scatter)")
+    p.add_argument("--crossover", action="store_true",
+                   help="diag: host calls at n = 1..256K frames on both sides of the CPU/GPU threshold "
+                        "(lvlip_csum_ctx_set_cpu_max), wall and CPU time per call")
     p.add_argument("--e2e", action="store_true",
                    help="also time the host-resident path (PCIe-inclusive; stderr + diag)")
     return p.parse_args(argv)
@@ -565,6 +568,8 @@ def run(args, world: int):
             diag["read_probe_GBps"] = read_probe(lvlip, torch, base, stream)
         if args.frames:
             diag["frames_dev"] = frames_dev(lvlip, torch, dev)
+        if args.frames or args.crossover:
+            diag["crossover"] = crossover(lvlip, dev)
         if args.e2e:
             diag["e2e_host_GBps"] = e2e(lvlip, b, base)
             diag["link_probe"] = link_probe(torch, dev, b.nbytes)
@@ -863,7 +868,7 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
     keep_slab = frames_arr(host, fd["offset"].astype(np.uint64))
     keep_scat = frames_arr(scat, slot.astype(np.uint64) * stride)
     d = dev.index or 0
-    with lvlip.Context(d) as ctx:
+    with lvlip.Context(d, cpu_max=0) as ctx:  # the GPU path (crossover() times both sides)
         run(ctx, keep_slab[1], "slab")
         run(ctx, keep_scat[1], "scattered")
         for tag, flag in (("dma", lvlip.REG_DMA), ("zerocopy", lvlip.REG_ZEROCOPY)):
@@ -878,7 +883,7 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
         k, v = env.split("=")
         os.environ[k] = v
         try:
-            with lvlip.Context(d) as ctx:
+            with lvlip.Context(d, cpu_max=0) as ctx:
                 if flag is not None:
                     ctx.register(host, flag)
                 try:
@@ -895,6 +900,182 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
         o, ln = int(fd["offset"][i]), int(fd["len"][i])
         assert np.array_equal(host[o:o + ln], scat[int(slot[i]) * stride:int(slot[i]) * stride + ln]), i
     return out
+
+
+def mixed_frames_host(lvlip, n):
+    """The mixed config's first n frames made valid IPv4/TCP/ICMP frames in
+    host memory (the same header fields mixed_frames_hbm writes): (uint8
+    array, FRAME_DESC_DTYPE descriptors)."""
+    import workloads
+
+    b = workloads.make("mixed", n=n)
+    host = b.host_bytes()
+    hdr, pay = b.descs[0::2], b.descs[1::2]
+    fs = (hdr["offset"] - 14).astype(np.int64)
+    iplen = (20 + pay["len"]).astype(np.int64)
+    for k, v in ((12, 0x08), (13, 0x00), (14, 0x45), (15, 0), (16, iplen >> 8), (17, iplen & 0xFF),
+                 (22, 64), (23, np.where(pay["start_sum"] != 0, 6, 1))):
+        host[fs + k] = v
+    fd = np.zeros(n, dtype=lvlip.FRAME_DESC_DTYPE)
+    fd["offset"] = fs
+    fd["len"] = 34 + pay["len"]
+    return host, fd
+
+
+CROSS_N = (1, 3, 8, 64, 512, 4096, 32768, 262144)
+SKB_DTYPE = np.dtype([("next", "<u8"), ("prev", "<u8"), ("rt", "<u8"), ("dev", "<u8"), ("refcnt", "<i4"),
+                      ("protocol", "<u2"), ("pad", "<u2"), ("len", "<u4"), ("dlen", "<u4"), ("seq", "<u4"),
+                      ("end_seq", "<u4"), ("end", "<u8"), ("head", "<u8"), ("data", "<u8"),
+                      ("payload", "<u8")])  # struct sk_buff on LP64 (include/skbuff.h:9-23)
+assert SKB_DTYPE.itemsize == 88 and SKB_DTYPE.fields["data"][1] == 72
+
+
+def crossover(lvlip, dev, ns=CROSS_N, budget_s=0.12):
+    """Where a context's host calls should leave the calling thread (VERDICT
+    r05 Next #1; lvlip_csum_ctx_set_cpu_max).  For n = 1 .. 256K of the mixed
+    config's frames, each host call is timed on both sides of the threshold in
+    the same context: "gpu" (cpu_max 0: the device pipeline) and "cpu"
+    (cpu_max 2^32-1: the library's CPU code on the calling thread, one core,
+    the drop-in checksum() per field).  Per call: wall time (us, the mean over
+    >= 3 calls after 2 warm-ups, including ~1 us of ctypes) and the process's
+    CPU time (us, every thread: the caller's wait and the pool's gather on the
+    GPU side).  Calls:
+      tx, rx_hdr, rx_l4   lvlip_tx_checksum, lvlip_rx_verify (flags 0, L4)
+      pkt_iov             lvlip_csum_batch_host over the frames' IPv4 headers
+                          and L4 segments (2n packets, what INTEGRATION §2a's
+                          per-field batch sends)
+      tx_skb, rx_skb      the _skb_list forms over sk_buff_heads of n skbs
+    Sources:
+      slab        the frames packed in one pageable buffer, in order
+      scattered   each frame at the start of its own alloc_skb(BUFLEN) slot
+                  (1616 B), the slots in shuffled order: netdev_rx_loop's /
+                  ip_output's skbs (src/netdev.c:86-101, src/skbuff.c:5-20)
+      registered  the slab registered LVLIP_REG_DMA (f3)
+    crossover[call/source] = the smallest n measured from which the GPU side's
+    wall time stays below the CPU side's (null: never up to 256K)."""
+    import ctypes
+
+    n_max = max(ns)
+    host, fd = mixed_frames_host(lvlip, n_max)
+    lib = lvlip.lib()
+    d = dev.index or 0
+    stride = 1616
+    rng = np.random.default_rng(9)
+    slot = rng.permutation(n_max)
+    scat = np.zeros(n_max * stride + 64, np.uint8)
+    for i in range(n_max):
+        o, ln = int(fd["offset"][i]), int(fd["len"][i])
+        scat[int(slot[i]) * stride:int(slot[i]) * stride + ln] = host[o:o + ln]
+    fr_dtype = np.dtype([("head", "<u8"), ("len", "<u4"), ("pad", "<u4")])
+    frames = {}
+    for tag, buf, offs in (("slab", host, fd["offset"].astype(np.uint64)),
+                           ("scattered", scat, slot.astype(np.uint64) * np.uint64(stride))):
+        fr = np.zeros(n_max, dtype=fr_dtype)
+        fr["head"] = np.uint64(buf.ctypes.data) + offs
+        fr["len"] = fd["len"]
+        frames[tag] = fr
+    frames["registered"] = frames["slab"]
+    # iov over the headers and L4 segments (2 per frame, frame order)
+    iovs = {}
+    for tag, fr in frames.items():
+        iov = np.zeros(2 * n_max, dtype=[("ptr", "<u8"), ("len", "<i4"), ("start_sum", "<u4")])
+        iov["ptr"][0::2] = fr["head"] + np.uint64(14)
+        iov["len"][0::2] = 20
+        iov["ptr"][1::2] = fr["head"] + np.uint64(34)
+        iov["len"][1::2] = fr["len"].astype(np.int64) - 34
+        iovs[tag] = iov
+    # skb queues over the scattered slots: RX as netdev_rx_loop leaves them
+    # (data at the frame, end = data + BUFLEN), TX as ip_output leaves them
+    # (data at the IPv4 header, len = the IP packet, 14 B reserved in front)
+    skbs = {}
+    for kind in ("rx", "tx"):
+        s = np.zeros(n_max, dtype=SKB_DTYPE)
+        a0 = s.ctypes.data
+        s["next"] = np.uint64(a0) + np.arange(1, n_max + 1, dtype=np.uint64) * np.uint64(88)
+        s["prev"] = np.uint64(a0) + (np.arange(n_max, dtype=np.uint64) - np.uint64(1)) * np.uint64(88)
+        fr = frames["scattered"]
+        if kind == "rx":
+            s["data"] = s["head"] = fr["head"]
+            s["end"] = fr["head"] + np.uint64(1600)
+        else:
+            s["head"] = fr["head"]
+            s["data"] = fr["head"] + np.uint64(14)
+            s["len"] = fr["len"] - 14
+            s["end"] = fr["head"] + np.uint64(stride)
+        skbs[kind] = s
+    qheads = {k: np.zeros(3, dtype=np.uint64) for k in skbs}  # struct sk_buff_head: next, prev, qlen
+    verdict = np.zeros(n_max, np.uint8)
+    outp = np.zeros(2 * n_max, np.uint16)
+    fp = {k: ctypes.cast(v.ctypes.data, ctypes.POINTER(lvlip.Frame)) for k, v in frames.items()}
+    ip = {k: ctypes.cast(v.ctypes.data, ctypes.POINTER(lvlip.Iov)) for k, v in iovs.items()}
+
+    def queue(kind, n):
+        """An sk_buff_head over the first n skbs of `kind` (list_add_tail order)."""
+        s, qh = skbs[kind], qheads[kind]
+        h = qh.ctypes.data
+        s["prev"][0] = h
+        s["next"][:n - 1] = np.uint64(s.ctypes.data) + np.arange(1, n, dtype=np.uint64) * np.uint64(88)
+        s["next"][n - 1] = h
+        qh[0], qh[1], qh[2] = s.ctypes.data, s.ctypes.data + 88 * (n - 1), n
+        return h
+
+    def timeit(call):
+        for _ in range(2):
+            r = call()
+            assert r >= 0, r
+        reps, t0, c0 = 0, time.perf_counter(), time.process_time()
+        while reps < 3 or time.perf_counter() - t0 < budget_s:
+            call()
+            reps += 1
+        return ((time.perf_counter() - t0) / reps * 1e6, (time.process_time() - c0) / reps * 1e6)
+
+    rows = {}
+    for tag in ("slab", "scattered", "registered"):
+        with lvlip.Context(d) as ctx:
+            if tag == "registered":
+                ctx.register(host, lvlip.REG_DMA)
+            try:
+                h, vp, op = ctx._h, verdict.ctypes.data, outp.ctypes.data
+                f_, i_ = fp[tag], ip[tag]
+                # each entry: n -> the call over the first n frames (queues built outside the timing)
+                calls = {
+                    "tx": lambda n: (lambda: lib.lvlip_tx_checksum(h, f_, n)),
+                    "rx_hdr": lambda n: (lambda: lib.lvlip_rx_verify(h, f_, n, 0, vp)),
+                    "rx_l4": lambda n: (lambda: lib.lvlip_rx_verify(h, f_, n, lvlip.RX_VERIFY_L4, vp)),
+                    "pkt_iov": lambda n: (lambda: lib.lvlip_csum_batch_host(h, i_, 2 * n, op)),
+                }
+                if tag == "scattered":
+                    def tx_skb(n):
+                        q = queue("tx", n)
+                        return lambda: lib.lvlip_tx_checksum_skb_list(h, q)
+
+                    def rx_skb(n):
+                        q = queue("rx", n)
+                        return lambda: lib.lvlip_rx_verify_skb_list(h, q, 0, vp, n_max)
+                    calls["tx_skb"], calls["rx_skb"] = tx_skb, rx_skb
+                for name, make_call in calls.items():
+                    r = {"gpu_us": [], "cpu_us": [], "gpu_cpu_time_us": [], "cpu_cpu_time_us": []}
+                    for n in ns:
+                        call = make_call(n)
+                        for side, cm in (("gpu", 0), ("cpu", 0xFFFFFFFF)):
+                            ctx.set_cpu_max(cm)
+                            w, c = timeit(call)
+                            r[f"{side}_us"].append(round(w, 2))
+                            r[f"{side}_cpu_time_us"].append(round(c, 2))
+                    rows[f"{name}/{tag}"] = r
+                    log(f"crossover {name}/{tag}: gpu {r['gpu_us']} cpu {r['cpu_us']}")
+            finally:
+                if tag == "registered":
+                    ctx.unregister(host)
+    cross = {}
+    for k, r in rows.items():
+        cross[k] = None
+        for j in range(len(ns)):
+            if all(g < c for g, c in zip(r["gpu_us"][j:], r["cpu_us"][j:])):
+                cross[k] = ns[j]
+                break
+    return {"n": list(ns), "frames": "mixed config (64-1460 B payloads, avg ~800 B frames)",
+            "rows": rows, "crossover": cross}
 
 
 def read_probe(lvlip, torch, base, stream):
@@ -1000,7 +1181,7 @@ def latency(lvlip, torch, dev):
             f()
         res[f"dev_n{n}_us"] = round((time.perf_counter() - t0) / 200 * 1e6, 1)
         host = b.host_bytes()
-        with lvlip.Context(dev.index or 0, arena_bytes=64 << 20) as ctx:
+        with lvlip.Context(dev.index or 0, arena_bytes=64 << 20, cpu_max=0) as ctx:
             for _ in range(20):
                 ctx.batch_host_flat(host, b.descs)
             t0 = time.perf_counter()
@@ -1033,7 +1214,7 @@ def e2e(lvlip, b, base):
     res = {}
     for name, flags in (("flat", None), ("registered_dma", lvlip.REG_DMA),
                         ("registered_zerocopy", lvlip.REG_ZEROCOPY), ("iov", None)):
-        with lvlip.Context(base.device.index or 0, arena_bytes=256 << 20) as ctx:
+        with lvlip.Context(base.device.index or 0, arena_bytes=256 << 20, cpu_max=0) as ctx:
             if flags is not None:
                 ctx.register(host, flags)
             if name == "iov":

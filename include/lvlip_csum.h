@@ -48,7 +48,11 @@ extern "C" {
  * (lvlip_partition_bytes, lvlip_csum_batch_host_flat_multi) and
  * lvlip_icmp_echo_reply_dev_ex (include/lvlip_skb.h).  INTEGRATION.md §5.
  * Round 5 changed no entry point: the host frame calls' implementation moved
- * to the device (include/lvlip_skb.h), with the same results. */
+ * to the device (include/lvlip_skb.h), with the same results.  Round 6 added
+ * entry points only (the size-based dispatch and its counters below, the
+ * context-free CPU frame calls of include/lvlip_skb.h); a context's host calls
+ * of at most LVLIP_CPU_MAX_DEFAULT packets / frames now run on the CPU by
+ * default, with identical results. */
 #define LVLIP_CSUM_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------- */
@@ -214,7 +218,9 @@ int lvlip_csum_batch_host(lvlip_csum_ctx *ctx, const lvlip_csum_iov *pkts,
                           uint32_t n, uint16_t *out);
 
 /* Same, for packets already laid out in one host buffer (descriptor
- * offsets relative to `base`, which must hold round_up(max end,16) bytes). */
+ * offsets relative to `base`, which must hold round_up(max end,16) bytes).
+ * Descriptors that cover their span densely and in order (see "densely"
+ * below) move as spans; others are gathered packet by packet. */
 int lvlip_csum_batch_host_flat(lvlip_csum_ctx *ctx, const void *base,
                                size_t base_bytes, const lvlip_csum_desc *d,
                                uint32_t n, uint16_t *out);
@@ -235,7 +241,15 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx *ctx, const void *base,
  *                       the span moves with the copy engine, as for
  *                       LVLIP_REG_DMA (faster: 2-5 % for packet batches,
  *                       ~20 % for the frame calls, whose per-frame parse reads
- *                       over PCIe)
+ *                       over PCIe).  Exception: the header-only
+ *                       lvlip_rx_verify (flags 0) needs 74 B of each frame
+ *                       and always reads a zero-copy region in place
+ * "Densely" means the packets' byte span is at most twice their bytes plus
+ * 1 MiB AND they come in address order: the sum of the jumps between
+ * consecutive start addresses is at most twice the span plus 1 MiB (a
+ * shuffled batch over a large slab would cut into pieces of one or two
+ * packets, each moving a whole span).  A DMA region's batch that is not dense
+ * is gathered packet by packet into the pinned arena.
  * Regions must not overlap; the memory must stay valid until unregistered
  * (lvlip_csum_ctx_destroy unregisters what is left).  Results are identical
  * on every path. */
@@ -243,6 +257,39 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx *ctx, const void *base,
 #define LVLIP_REG_ZEROCOPY 1u
 int lvlip_csum_register(lvlip_csum_ctx *ctx, void *ptr, size_t bytes, uint32_t flags);
 int lvlip_csum_unregister(lvlip_csum_ctx *ctx, void *ptr);
+
+/* Size-based dispatch of the host calls (SURVEY.md §5 "Config/flags", §7
+ * step 5).  A host call over at most cpu_max packets (lvlip_csum_batch_host,
+ * lvlip_csum_batch_host_flat) or frames (lvlip_rx_verify, lvlip_tx_checksum
+ * and their _skb_list forms, include/lvlip_skb.h) runs on the CALLING THREAD
+ * with the library's own CPU code (Group 1's checksum(); lvlip_rx_verify_cpu /
+ * lvlip_tx_checksum_cpu), never touching the GPU: a GPU round trip costs a
+ * host call ~20 us before the first byte is summed, more than one core needs
+ * for level-ip's usual flushes of 1-30 frames (DESIGN.md §9 measures the
+ * crossover).  This is a performance choice only: results, return codes and
+ * the untouched-on-error rule are identical on both sides of the threshold
+ * (the GPU tests check both).  It is distinct from the error rule above: a
+ * call that goes to the GPU and fails still returns LVLIP_E* with no CPU
+ * substitute.  0 = every call goes to the GPU.  The default is the env var
+ * LVLIP_CPU_MAX when set when the context is created, else
+ * LVLIP_CPU_MAX_DEFAULT.  Device-resident calls (Groups 2 and the _dev frame
+ * calls) are never dispatched to the CPU. */
+#define LVLIP_CPU_MAX_DEFAULT 2048u
+int lvlip_csum_ctx_set_cpu_max(lvlip_csum_ctx *ctx, uint32_t cpu_max);
+/* The context's current threshold (0 for a NULL context). */
+uint32_t lvlip_csum_ctx_cpu_max(const lvlip_csum_ctx *ctx);
+
+/* Counters of a context since it was created (for tests, benches and a
+ * maintainer's own monitoring). */
+typedef struct lvlip_ctx_stats {
+    uint64_t gpu_calls;  /* host calls that ran on the GPU                  */
+    uint64_t cpu_calls;  /* host calls run on the calling thread (cpu_max)  */
+    uint64_t pieces;     /* device pieces launched by the GPU calls         */
+    uint64_t h2d_bytes;  /* packet / frame bytes copied host->device by the
+                            copy engine (descriptors and in-place reads over
+                            PCIe not counted)                              */
+} lvlip_ctx_stats;
+int lvlip_csum_ctx_stats(const lvlip_csum_ctx *ctx, lvlip_ctx_stats *out);
 
 /* ======================================================================= */
 /* Group 4: one batch over several GPUs                     */

@@ -146,6 +146,25 @@ int lvlip_rx_verify_skb_list(lvlip_csum_ctx *ctx, struct sk_buff_head *q, uint32
  * LVLIP_E* (skbs untouched on error). */
 int lvlip_tx_checksum_skb_list(lvlip_csum_ctx *ctx, struct sk_buff_head *q);
 
+/* ---- f1/f2 on the calling thread (no context, no GPU) --------------------- */
+
+/* The same calls computed by the library's CPU code on the calling thread,
+ * with the same results and return codes (LVLIP_EINVAL on a malformed frame,
+ * frames untouched; no arena, so never LVLIP_ERANGE).  A context's calls of at
+ * most its cpu_max frames run these (lvlip_csum_ctx_set_cpu_max,
+ * include/lvlip_csum.h).  A caller that deferred its TX checksums also calls
+ * them when the GPU call fails (LVLIP_ENODEV, LVLIP_EHIP, LVLIP_ENOMEM,
+ * LVLIP_ERANGE; or no context could be made), so that no frame leaves with a
+ * deferred, still-zero field (src/ip_output.c:53-55 sends
+ * whatever the fields hold).  Reentrant; one checksum() per field, as the
+ * reference's call sites. */
+int lvlip_rx_verify_cpu(const lvlip_frame *frames, uint32_t n, uint32_t flags,
+                        uint8_t *verdict);
+int lvlip_tx_checksum_cpu(lvlip_frame *frames, uint32_t n);
+int lvlip_rx_verify_skb_list_cpu(struct sk_buff_head *q, uint32_t flags,
+                                 uint8_t *verdict, uint32_t cap);
+int lvlip_tx_checksum_skb_list_cpu(struct sk_buff_head *q);
+
 /* ---- f1/f2/f4 on device-resident frames ---------------------------------- */
 
 /* Frames already in HBM (a receive ring filled by a GPU-direct NIC, or frames

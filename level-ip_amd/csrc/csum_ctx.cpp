@@ -59,6 +59,13 @@ int drain(lvlip_csum_ctx* c, Slot& s) {
     return LVLIP_OK;
 }
 
+int count_piece(lvlip_csum_ctx* c) {
+    c->stats.pieces++;
+    if (c->fail_piece && ++c->call_pieces == c->fail_piece)
+        return fail(c, hipErrorLaunchFailure, "injected failure (LVLIP_FAIL_PIECE)");
+    return LVLIP_OK;
+}
+
 int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes, uint64_t piece_bytes) {
     const hipError_t e = hipEventRecord(s.done, s.stream);
     if (e != hipSuccess) return fail(c, e, "hipEventRecord");
@@ -135,6 +142,7 @@ void free_slot(Slot& s) {
 int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uint16_t* user_out,
                  const uint8_t* src = nullptr, const uint8_t* dev_base = nullptr) {
     hipError_t e;
+    if (const int rc = count_piece(c); rc != LVLIP_OK) return rc;
     lvlip_launch_cfg cfg{};
     cfg.kernel = LVLIP_KERNEL_AUTO;  // the piece's average length picks the kernel
     cfg.len_hint = (int32_t)(bytes / count > 0x7fffffffull ? 0x7fffffff : bytes / count);
@@ -163,6 +171,7 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
         const uint64_t nb = src && src != s.h_bytes ? bytes : align16(bytes);
         const int rc = h2d_ordered(c, s, s.d_bytes, src ? src : s.h_bytes, nb, "H2D bytes");
         if (rc != LVLIP_OK) return rc;
+        c->stats.h2d_bytes += nb;
     }
     int rc = lvlip_csum_batch_dev_ex(dev_base ? dev_base : s.d_bytes, s.d_desc, count, s.d_out,
                                      s.stream, &cfg);
@@ -195,36 +204,9 @@ int first_failure(lvlip_csum_ctx* c, uint32_t n, const F& check) {
     return f == ~0ull ? LVLIP_OK : -(int)(f & 0xffu);
 }
 
-// Whether n packets (start address off_of(q), length len_of(q)) cover their
-// byte span densely: the span at most twice their bytes plus 1 MiB, the frame
-// calls' rule; on the pool threads.
-template <class Off, class Len>
-bool dense_span(lvlip_csum_ctx* c, uint32_t n, const Off& off_of, const Len& len_of) {
-    std::atomic<uint64_t> lo{~0ull}, hi{0}, sum{0};
-    parallel_ranges(c, n, 65536, [&](uint64_t a, uint64_t z) {
-        uint64_t l = ~0ull, h = 0, t = 0;
-        for (uint64_t q = a; q < z; ++q) {
-            const int32_t sl = len_of((uint32_t)q);
-            if (sl <= 0) continue;
-            const uint64_t o = off_of((uint32_t)q), e = o + (uint64_t)sl;
-            l = o < l ? o : l;
-            h = e > h ? e : h;
-            t += (uint64_t)sl;
-        }
-        uint64_t cur = lo.load(std::memory_order_relaxed);
-        while (l < cur && !lo.compare_exchange_weak(cur, l, std::memory_order_relaxed)) {
-        }
-        cur = hi.load(std::memory_order_relaxed);
-        while (h > cur && !hi.compare_exchange_weak(cur, h, std::memory_order_relaxed)) {
-        }
-        sum.fetch_add(t, std::memory_order_relaxed);
-    });
-    const uint64_t l = lo.load(), h = hi.load();
-    return h > l && h - l <= 2 * sum.load() + (1ull << 20);
-}
-
 // The context's scratch array for the host batch calls, at least `bytes`
-// (kept across calls: fresh pages would fault on every call).
+// (kept across calls: fresh pages would fault on every call; trim_scratch
+// releases one above kScratchKeep when the call ends).
 void* host_scratch(lvlip_csum_ctx* c, size_t bytes) {
     if (c->host_scratch_bytes < bytes) {
         free(c->host_scratch);
@@ -232,6 +214,70 @@ void* host_scratch(lvlip_csum_ctx* c, size_t bytes) {
         c->host_scratch_bytes = c->host_scratch ? bytes : 0;
     }
     return c->host_scratch;
+}
+
+// The packets of a host call on the calling thread (cpu_max): Group 1's
+// checksum() per packet, the reference's own arithmetic (src/utils.c:40-55).
+template <class Ptr, class Len, class Seed>
+int cpu_batch(lvlip_csum_ctx* c, uint32_t n, uint16_t* out, const Ptr& ptr_of, const Len& len_of,
+              const Seed& seed_of) {
+    c->stats.cpu_calls++;
+    for (uint32_t q = 0; q < n; ++q) {
+        const int32_t l = len_of(q);
+        out[q] = checksum(l > 0 ? (void*)ptr_of(q) : nullptr, l, (int)seed_of(q));
+    }
+    return LVLIP_OK;
+}
+
+// Gathers n packets (ptr_of, len_of, seed_of) into the pinned arena, each at
+// the next 16-B aligned offset, piece by piece over the two slots (the
+// scattered path of lvlip_csum_batch_host, and the flat call's path for
+// descriptors that do not cover their span densely in order).  Every packet
+// fits the arena (checked by the callers).
+template <class Ptr, class Len, class Seed>
+int gather_batch(lvlip_csum_ctx* c, uint32_t n, uint16_t* out, const Ptr& ptr_of, const Len& len_of,
+                 const Seed& seed_of) {
+    int cur = 0;
+    uint32_t i = 0;
+    int rc = LVLIP_OK;
+    while (i < n && rc == LVLIP_OK) {
+        Slot& s = c->slot[cur];
+        if ((rc = drain(c, s)) != LVLIP_OK) break;
+        // lay out a piece: packet k at the next 16-B aligned offset ...
+        uint64_t off = 0;
+        uint32_t k = 0;
+        const uint32_t first = i;
+        while (i < n && k < c->max_desc) {
+            const int32_t len = len_of(i);
+            const uint64_t need = len > 0 ? (uint64_t)len : 0;
+            if (off + need > (k ? c->piece : c->arena)) break;
+            s.h_desc[k].offset = off;
+            s.h_desc[k].len = len;
+            s.h_desc[k].start_sum = seed_of(i);
+            off = align16(off + need);
+            ++k;
+            ++i;
+        }
+        // ... then gather the bytes, packets split over the host threads,
+        // nontemporal stores (copy_nt), the next packets prefetched
+        {
+            uint8_t* dst = s.h_bytes;
+            const lvlip_csum_desc* hd = s.h_desc;
+            parallel_ranges(c, k, 1024, [=](uint64_t lo, uint64_t hi) {
+                for (uint64_t q = lo; q < hi; ++q) {
+                    if (q + 8 < hi && hd[q + 8].len > 0)
+                        for (int32_t l = 0; l < hd[q + 8].len; l += 64)
+                            __builtin_prefetch((const uint8_t*)ptr_of(first + (uint32_t)q + 8) + l);
+                    if (hd[q].len > 0)
+                        copy_nt(dst + hd[q].offset, (const uint8_t*)ptr_of(first + (uint32_t)q), (uint64_t)hd[q].len);
+                }
+                _mm_sfence();
+            });
+        }
+        rc = launch_piece(c, s, off ? off : 16, k, out + first);
+        cur ^= 1;
+    }
+    return finish_pieces(c, rc);
 }
 
 // Zero-copy: descriptors only (offsets from the region's first byte rounded
@@ -272,6 +318,94 @@ int zerocopy_batch(lvlip_csum_ctx* c, const Region& r, uint32_t n, uint16_t* out
             }
         });
         rc = launch_piece(c, s, bytes ? bytes : 16, k, out + first, nullptr, d0);
+        cur ^= 1;
+    }
+    return finish_pieces(c, rc);
+}
+
+// lvlip_csum_batch_host_flat's GPU path over validated descriptors.  dense:
+// 1 / 0 when the caller has scanned the batch (dense_ordered's rule), -1 to
+// scan here.  Dense batches move their spans (the copy engine straight from a
+// registered region, else one nontemporal copy per span into the pinned
+// arena); other batches are read in place from a zero-copy region, or
+// gathered packet by packet.
+int host_flat_impl(lvlip_csum_ctx* c, const uint8_t* b, size_t base_bytes, const lvlip_csum_desc* d, uint32_t n,
+                   uint16_t* out, int dense) {
+    const Region* reg = c->regions.empty() ? nullptr : find_region(c, b, base_bytes);
+    if (dense < 0)
+        dense = dense_ordered(
+            c, n, [b, d](uint32_t q) { return (uint64_t)(uintptr_t)(b + d[q].offset); },
+            [d](uint32_t q) { return d[q].len; });
+    if (!dense) {
+        if (reg && (reg->flags & LVLIP_REG_ZEROCOPY))
+            return zerocopy_batch(
+                c, *reg, n, out, [&](uint32_t q) { return b + d[q].offset; }, [&](uint32_t q) { return d[q]; },
+                [&](uint32_t q) { return d[q].len; });
+        // every packet fits the arena: the flat call's rule is the stricter
+        return gather_batch(
+            c, n, out, [b, d](uint32_t q) { return b + d[q].offset; }, [d](uint32_t q) { return d[q].len; },
+            [d](uint32_t q) { return d[q].start_sum; });
+    }
+    // a piece's bytes: from a registered region the whole arena (no gather to
+    // overlap with the copies, and each copy costs the copy engine ~18 us
+    // between pieces: DESIGN.md §5), else LVLIP_PIECE_MAX.  A dense batch in
+    // a zero-copy region moves its spans as from a DMA region (tcp1500:
+    // 54.6-55.2 against 52.5 GB/s in place)
+    const uint64_t limit = reg ? c->arena : c->piece;
+    int cur = 0;
+    uint32_t i = 0;
+    int rc = LVLIP_OK;
+    while (i < n && rc == LVLIP_OK) {
+        Slot& s = c->slot[cur];
+        if ((rc = drain(c, s)) != LVLIP_OK) break;
+        // A piece is a run of descriptors whose byte span [lo16, hi) fits the
+        // arena.  The span is copied with one memcpy, keeping each packet's
+        // offset mod 16 (so odd/unaligned starts stay exactly as given).
+        const uint32_t first = i;
+        uint64_t lo16 = ~0ull, hi = 0;
+        uint32_t k = 0;
+        while (i < n && k < c->max_desc) {
+            const uint64_t o = d[i].offset;
+            const uint64_t e = o + (d[i].len > 0 ? (uint64_t)d[i].len : 0);
+            const uint64_t nlo = (o & ~15ull) < lo16 ? (o & ~15ull) : lo16;
+            const uint64_t nhi = e > hi ? e : hi;
+            // k >= 1 here: a single span always fits the arena (checked by the caller)
+            if (align16(nhi) - nlo > (k ? limit : c->arena)) break;
+            lo16 = nlo;
+            hi = nhi;
+            ++k;
+            ++i;
+        }
+        const uint64_t span = hi > lo16 ? hi - lo16 : 0;
+        const uint8_t* from = nullptr;
+        if (span && reg) {
+            // f3 DMA: the copy engine reads the registered span directly.  Its
+            // last bytes up to the next 16 B may lie past base_bytes, so copy
+            // exactly `span` and let the kernel's 16-B tail read the arena.
+            from = b + lo16;
+        } else if (span) {
+            // the span in 64-B blocks over the threads, nontemporal stores
+            uint8_t* dst = s.h_bytes;
+            const uint8_t* src = b + lo16;
+            const uint64_t nblk = (span + 63) / 64;
+            parallel_ranges(c, nblk, 8192, [=](uint64_t lo, uint64_t hi) {
+                const uint64_t e = hi * 64 < span ? hi * 64 : span;
+                copy_nt(dst + lo * 64, src + lo * 64, e - lo * 64);
+                _mm_sfence();
+            });
+        }
+        {
+            lvlip_csum_desc* hd = s.h_desc;
+            const lvlip_csum_desc* src = d + first;
+            const uint64_t base16 = lo16;
+            parallel_ranges(c, k, 16384, [hd, src, base16](uint64_t lo, uint64_t hi) {
+                for (uint64_t q = lo; q < hi; ++q) {
+                    hd[q] = src[q];
+                    hd[q].offset = src[q].offset - base16;
+                }
+            });
+        }
+        rc = launch_piece(c, s, span ? span : 16, k, out + first, from);
         cur ^= 1;
     }
     return finish_pieces(c, rc);
@@ -323,6 +457,19 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         const char* e = getenv("LVLIP_FIRST_PIECE");
         const long long v = e ? atoll(e) : 0;
         c->first_piece = v > 0 ? align16((uint64_t)v) : (4ull << 20);
+        if (c->first_piece > c->piece) c->first_piece = c->piece;  // the ramp's shifts never overflow
+    }
+    // LVLIP_CPU_MAX: host calls of at most this many packets / frames run on
+    // the calling thread (lvlip_csum_ctx_set_cpu_max; 0: always the GPU)
+    {
+        const char* e = getenv("LVLIP_CPU_MAX");
+        const long long v = e ? atoll(e) : (long long)LVLIP_CPU_MAX_DEFAULT;
+        c->cpu_max = v > 0 ? (uint32_t)(v > 0xffffffffll ? 0xffffffffll : v) : 0u;
+    }
+    {
+        const char* e = getenv("LVLIP_FAIL_PIECE");
+        const long long v = e ? atoll(e) : 0;
+        c->fail_piece = v > 0 ? (uint32_t)(v > 0xffffffffll ? 0xffffffffll : v) : 0u;
     }
     // LVLIP_BLOCK_MIN: a piece of at least this many bytes is waited for by
     // polling between short sleeps instead of by spinning: the pipeline's
@@ -387,6 +534,20 @@ int lvlip_csum_ctx_destroy(lvlip_csum_ctx* c) {
     return LVLIP_OK;
 }
 
+int lvlip_csum_ctx_set_cpu_max(lvlip_csum_ctx* c, uint32_t cpu_max) {
+    if (!c) return LVLIP_EINVAL;
+    c->cpu_max = cpu_max;
+    return LVLIP_OK;
+}
+
+uint32_t lvlip_csum_ctx_cpu_max(const lvlip_csum_ctx* c) { return c ? c->cpu_max : 0u; }
+
+int lvlip_csum_ctx_stats(const lvlip_csum_ctx* c, lvlip_ctx_stats* out) {
+    if (!c || !out) return LVLIP_EINVAL;
+    *out = c->stats;
+    return LVLIP_OK;
+}
+
 int lvlip_csum_register(lvlip_csum_ctx* c, void* ptr, size_t bytes, uint32_t flags) {
     if (!c || !ptr || bytes == 0 || flags > LVLIP_REG_ZEROCOPY) return LVLIP_EINVAL;
     uint8_t* p = (uint8_t*)ptr;
@@ -437,122 +598,80 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
     if (first_failure(c, n, [pkts](uint32_t i) { return pkts[i].len > 0 && !pkts[i].ptr ? LVLIP_EINVAL : LVLIP_OK; }) !=
         LVLIP_OK)
         return LVLIP_EINVAL;
-    DeviceGuard g(c->device);
-    if (!c->regions.empty()) {
-        // f3: all packets inside one registered region (the region of the
-        // first non-empty packet; regions never overlap) -> no gather at all:
-        // packets that cover their span densely go as a flat batch over the
-        // region (the copy engine moves the spans); a zero-copy region's
-        // sparse packets are read in place; a DMA region's sparse ones are
-        // gathered below
-        uint32_t i0 = 0;
-        while (i0 < n && pkts[i0].len <= 0) ++i0;
-        const Region* r = i0 < n ? find_region(c, pkts[i0].ptr, (uint64_t)pkts[i0].len) : nullptr;
-        // one pass on the pool threads: every packet inside r, the packets'
-        // span and bytes (dense?), and their flat descriptors relative to r
-        // (written whether or not they are used)
-        bool inside = false, dense = false;
-        lvlip_csum_desc* fd = nullptr;
-        if (r) {
-            fd = (lvlip_csum_desc*)host_scratch(c, sizeof(lvlip_csum_desc) * (size_t)n);
-            const uint8_t *r0 = r->host, *r1 = r->host + r->bytes;
-            std::atomic<bool> outside{false};
-            std::atomic<uint64_t> lo{~0ull}, hi{0}, sum{0};
-            parallel_ranges(c, n, 65536, [&, fd, r0, r1](uint64_t a, uint64_t z) {
-                uint64_t l = ~0ull, h = 0, t = 0;
-                for (uint64_t q = a; q < z; ++q) {
-                    const int32_t len = pkts[q].len;
-                    uint64_t o = 0;
-                    if (len > 0) {
-                        const uint8_t* p = (const uint8_t*)pkts[q].ptr;
-                        if (p < r0 || p + len > r1) {
-                            outside.store(true, std::memory_order_relaxed);
-                            return;
-                        }
-                        o = (uint64_t)(p - r0);
-                        l = o < l ? o : l;
-                        h = o + (uint64_t)len > h ? o + (uint64_t)len : h;
-                        t += (uint64_t)len;
-                    }
-                    if (fd) fd[q] = lvlip_csum_desc{o, len, pkts[q].start_sum};
-                }
-                uint64_t cur = lo.load(std::memory_order_relaxed);
-                while (l < cur && !lo.compare_exchange_weak(cur, l, std::memory_order_relaxed)) {
-                }
-                cur = hi.load(std::memory_order_relaxed);
-                while (h > cur && !hi.compare_exchange_weak(cur, h, std::memory_order_relaxed)) {
-                }
-                sum.fetch_add(t, std::memory_order_relaxed);
-            });
-            inside = !outside.load();
-            const uint64_t l = lo.load(), h = hi.load();
-            dense = inside && h > l && h - l <= 2 * sum.load() + (1ull << 20);
-        }
-        if (dense && fd) {
-            // refused only when one packet's 16-B span exceeds the arena (the
-            // flat call's rule): then the gather below takes it
-            const int frc = lvlip_csum_batch_host_flat(c, r->host, r->bytes, fd, n, out);
-            if (frc != LVLIP_ERANGE) return frc;
-        }
-        if (inside && (r->flags & LVLIP_REG_ZEROCOPY))
-            return zerocopy_batch(
-                c, *r, n, out,
-                [&](uint32_t q) { return pkts[q].len > 0 ? (const uint8_t*)pkts[q].ptr : r->host; },
-                [&](uint32_t q) {
-                    lvlip_csum_desc d{};
-                    d.len = pkts[q].len;
-                    d.start_sum = pkts[q].start_sum;
-                    return d;
-                },
-                [&](uint32_t q) { return pkts[q].len; });
-    }
     const uint64_t arena = c->arena;
     if (first_failure(c, n, [pkts, arena](uint32_t i) {
             return pkts[i].len > 0 && align16((uint64_t)pkts[i].len) > arena ? LVLIP_ERANGE : LVLIP_OK;
         }) != LVLIP_OK)
-        return LVLIP_ERANGE;  // a single packet larger than the arena
-
-    int cur = 0;
-    uint32_t i = 0;
-    int rc = LVLIP_OK;
-    while (i < n && rc == LVLIP_OK) {
-        Slot& s = c->slot[cur];
-        if ((rc = drain(c, s)) != LVLIP_OK) break;
-        // lay out a piece: packet k at the next 16-B aligned offset ...
-        uint64_t off = 0;
-        uint32_t k = 0;
-        const uint32_t first = i;
-        while (i < n && k < c->max_desc) {
-            const int32_t len = pkts[i].len;
-            const uint64_t need = len > 0 ? (uint64_t)len : 0;
-            if (off + need > (k ? c->piece : c->arena)) break;
-            s.h_desc[k].offset = off;
-            s.h_desc[k].len = len;
-            s.h_desc[k].start_sum = pkts[i].start_sum;
-            off = align16(off + need);
-            ++k;
-            ++i;
-        }
-        // ... then gather the bytes, packets split over the host threads,
-        // nontemporal stores (copy_nt), the next packets prefetched
-        {
-            uint8_t* dst = s.h_bytes;
-            const lvlip_csum_desc* hd = s.h_desc;
-            const lvlip_csum_iov* src = pkts + first;
-            parallel_ranges(c, k, 1024, [=](uint64_t lo, uint64_t hi) {
-                for (uint64_t q = lo; q < hi; ++q) {
-                    if (q + 8 < hi && hd[q + 8].len > 0)
-                        for (int32_t l = 0; l < hd[q + 8].len; l += 64)
-                            __builtin_prefetch((const uint8_t*)src[q + 8].ptr + l);
-                    if (hd[q].len > 0) copy_nt(dst + hd[q].offset, (const uint8_t*)src[q].ptr, (uint64_t)hd[q].len);
+        return LVLIP_ERANGE;  // a single packet larger than the arena (on every path)
+    auto ptr_of = [pkts](uint32_t q) { return (const uint8_t*)pkts[q].ptr; };
+    auto len_of = [pkts](uint32_t q) { return pkts[q].len; };
+    auto seed_of = [pkts](uint32_t q) { return pkts[q].start_sum; };
+    if (n <= c->cpu_max) return cpu_batch(c, n, out, ptr_of, len_of, seed_of);
+    DeviceGuard g(c->device);
+    begin_gpu_call(c);
+    int rc = LVLIP_ERANGE;  // "not handled by a region path yet"
+    if (!c->regions.empty()) {
+        // f3: all packets inside one registered region (the region of the
+        // first non-empty packet; regions never overlap) -> no gather at all:
+        // packets that cover their span densely and in order go as a flat
+        // batch over the region (the copy engine moves the spans); a
+        // zero-copy region's other batches are read in place; a DMA region's
+        // are gathered below
+        uint32_t i0 = 0;
+        while (i0 < n && pkts[i0].len <= 0) ++i0;
+        const Region* r = i0 < n ? find_region(c, pkts[i0].ptr, (uint64_t)pkts[i0].len) : nullptr;
+        if (r) {
+            // one pass on the pool threads: every packet inside r, the
+            // packets' span, bytes and jumps (dense_ordered's scan), and
+            // their flat descriptors relative to r (written whether or not
+            // they are used; the array is trimmed after a huge call)
+            lvlip_csum_desc* fd = (lvlip_csum_desc*)host_scratch(c, sizeof(lvlip_csum_desc) * (size_t)n);
+            const uint8_t *r0 = r->host, *r1 = r->host + r->bytes;
+            std::atomic<bool> outside{false};
+            constexpr uint32_t kParts = 256;
+            SpanScan part[kParts];
+            const uint32_t np = n / 4096u < 1u ? 1u : (n / 4096u > kParts ? kParts : n / 4096u);
+            parallel_ranges(c, np, 1, [&, fd, r0, r1](uint64_t plo, uint64_t phi) {
+                for (uint64_t j = plo; j < phi; ++j) {
+                    SpanScan sc;
+                    const uint32_t a = (uint32_t)((uint64_t)n * j / np), z = (uint32_t)((uint64_t)n * (j + 1) / np);
+                    for (uint32_t q = a; q < z; ++q) {
+                        const int32_t len = pkts[q].len;
+                        uint64_t o = 0;
+                        if (len > 0) {
+                            const uint8_t* p = (const uint8_t*)pkts[q].ptr;
+                            if (p < r0 || p + len > r1) {
+                                outside.store(true, std::memory_order_relaxed);
+                                return;
+                            }
+                            o = (uint64_t)(p - r0);
+                            span_add(sc, o, (uint64_t)len);
+                        }
+                        if (fd) fd[q] = lvlip_csum_desc{o, len, pkts[q].start_sum};
+                    }
+                    part[j] = sc;
                 }
-                _mm_sfence();
             });
+            const bool inside = !outside.load();
+            if (inside && fd && span_dense(span_merge(part, np)))
+                // refused only when one packet's 16-B span exceeds the arena
+                // (the flat call's rule): then the gather below takes it
+                rc = host_flat_impl(c, r->host, r->bytes, fd, n, out, 1);
+            else if (inside && (r->flags & LVLIP_REG_ZEROCOPY))
+                rc = zerocopy_batch(
+                    c, *r, n, out, [&](uint32_t q) { return pkts[q].len > 0 ? (const uint8_t*)pkts[q].ptr : r->host; },
+                    [&](uint32_t q) {
+                        lvlip_csum_desc d{};
+                        d.len = pkts[q].len;
+                        d.start_sum = pkts[q].start_sum;
+                        return d;
+                    },
+                    [&](uint32_t q) { return pkts[q].len; });
         }
-        rc = launch_piece(c, s, off ? off : 16, k, out + first);
-        cur ^= 1;
     }
-    return finish_pieces(c, rc);
+    if (rc == LVLIP_ERANGE) rc = gather_batch(c, n, out, ptr_of, len_of, seed_of);
+    trim_scratch(c);
+    return rc;
 }
 
 int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_bytes,
@@ -570,78 +689,15 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
         return LVLIP_OK;
     });
     if (bad != LVLIP_OK) return bad;
+    if (n <= c->cpu_max)
+        return cpu_batch(
+            c, n, out, [b, d](uint32_t q) { return b + d[q].offset; }, [d](uint32_t q) { return d[q].len; },
+            [d](uint32_t q) { return d[q].start_sum; });
     DeviceGuard g(c->device);
-    const Region* reg = c->regions.empty() ? nullptr : find_region(c, b, base_bytes);
-    // a zero-copy region is read in place, unless the batch covers its span
-    // densely: then the copy engine moves the spans as from a DMA region
-    // (tcp1500: 54.6-55.2 against 52.5 GB/s in place)
-    if (reg && (reg->flags & LVLIP_REG_ZEROCOPY) &&
-        !dense_span(c, n, [d](uint32_t q) { return d[q].offset; }, [d](uint32_t q) { return d[q].len; }))
-        return zerocopy_batch(
-            c, *reg, n, out, [&](uint32_t q) { return b + d[q].offset; },
-            [&](uint32_t q) { return d[q]; }, [&](uint32_t q) { return d[q].len; });
-
-    // a piece's bytes: from a DMA region the whole arena (no gather to
-    // overlap with the copies, and each copy costs the copy engine ~18 us
-    // between pieces: DESIGN.md §5), else LVLIP_PIECE_MAX
-    const uint64_t limit = reg ? c->arena : c->piece;
-    int cur = 0;
-    uint32_t i = 0;
-    int rc = LVLIP_OK;
-    while (i < n && rc == LVLIP_OK) {
-        Slot& s = c->slot[cur];
-        if ((rc = drain(c, s)) != LVLIP_OK) break;
-        // A piece is a run of descriptors whose byte span [lo16, hi) fits the
-        // arena.  The span is copied with one memcpy, keeping each packet's
-        // offset mod 16 (so odd/unaligned starts stay exactly as given).
-        const uint32_t first = i;
-        uint64_t lo16 = ~0ull, hi = 0;
-        uint32_t k = 0;
-        while (i < n && k < c->max_desc) {
-            const uint64_t o = d[i].offset;
-            const uint64_t e = o + (d[i].len > 0 ? (uint64_t)d[i].len : 0);
-            const uint64_t nlo = (o & ~15ull) < lo16 ? (o & ~15ull) : lo16;
-            const uint64_t nhi = e > hi ? e : hi;
-            // k >= 1 here: a single span always fits the arena (checked above)
-            if (align16(nhi) - nlo > (k ? limit : c->arena)) break;
-            lo16 = nlo;
-            hi = nhi;
-            ++k;
-            ++i;
-        }
-        const uint64_t span = hi > lo16 ? hi - lo16 : 0;
-        const uint8_t* from = nullptr;
-        if (span && reg) {
-            // f3 DMA: the copy engine reads the registered span directly.  Its
-            // last bytes up to the next 16 B may lie past base_bytes, so copy
-            // exactly `span` and let the kernel's 16-B tail read the arena.
-            from = b + lo16;
-        } else if (span) {
-            // the span in 64-B blocks over the threads, nontemporal stores
-            uint8_t* dst = s.h_bytes;
-            const uint8_t* src = b + lo16;
-            const uint64_t nblk = (span + 63) / 64;
-            parallel_ranges(c, nblk, 8192, [=](uint64_t lo, uint64_t hi) {
-                const uint64_t e = hi * 64 < span ? hi * 64 : span;
-                copy_nt(dst + lo * 64, src + lo * 64, e - lo * 64);
-                _mm_sfence();
-            });
-        }
-        {
-            lvlip_csum_desc* hd = s.h_desc;
-            const lvlip_csum_desc* src = d + first;
-            const uint64_t base16 = lo16;
-            parallel_ranges(c, k, 16384, [hd, src, base16](uint64_t lo, uint64_t hi) {
-                for (uint64_t q = lo; q < hi; ++q) {
-                    hd[q] = src[q];
-                    hd[q].offset = src[q].offset - base16;
-                }
-            });
-        }
-        rc = launch_piece(c, s, span ? span : 16, k, out + first, from);
-        cur ^= 1;
-    }
-    return finish_pieces(c, rc);
+    begin_gpu_call(c);
+    const int rc = host_flat_impl(c, b, base_bytes, d, n, out, -1);
+    trim_scratch(c);
+    return rc;
 }
 
 // Group 4: one host thread per context, each on its part of the batch.  The

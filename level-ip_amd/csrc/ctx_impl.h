@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -93,6 +94,15 @@ struct lvlip_csum_ctx {
     void* host_scratch = nullptr;
     size_t host_scratch_bytes = 0;
     int frame_trace = 0;      // LVLIP_FRAME_TRACE=1: per-step host times on stderr
+    // host calls of at most this many packets / frames run on the calling
+    // thread (lvlip_csum_ctx_set_cpu_max; 0: never)
+    uint32_t cpu_max = LVLIP_CPU_MAX_DEFAULT;
+    lvlip_ctx_stats stats{};
+    // test hook LVLIP_FAIL_PIECE=k (k >= 1): the k-th device piece of every GPU
+    // call fails with LVLIP_EHIP before it is launched, so the tests can drive
+    // the error paths (a TX call's undo, a caller's CPU fill) on a healthy GPU
+    uint32_t fail_piece = 0;
+    uint32_t call_pieces = 0;  // pieces launched by the current call
     lvlip_ctx::Slot slot[lvlip_ctx::kSlots];
     std::vector<lvlip_ctx::Region> regions;
     lvlip::GatherPool pool;
@@ -117,6 +127,74 @@ const Region* find_region(const lvlip_csum_ctx* c, const void* p, uint64_t len);
 // records the slot's completion after its piece of `piece_bytes` bytes; the
 // wait for it sleeps from c->block_min bytes up, else spins
 int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes, uint64_t piece_bytes);
+// Counts a device piece of the current call (stats, LVLIP_FAIL_PIECE):
+// LVLIP_OK, or the injected LVLIP_EHIP.
+int count_piece(lvlip_csum_ctx* c);
+// Start of a host call that goes to the GPU (counters, the per-call piece count).
+inline void begin_gpu_call(lvlip_csum_ctx* c) {
+    c->stats.gpu_calls++;
+    c->call_pieces = 0;
+}
+
+// The per-call host arrays are kept for the next call (fresh pages would fault
+// on every call), except one above this size, released when its call ends so
+// that one huge batch does not hold memory for the context's lifetime
+// (the iov call's 16 n bytes of flat descriptors).
+constexpr size_t kScratchKeep = 64ull << 20;
+inline void trim_scratch(lvlip_csum_ctx* c) {
+    auto trim = [](void*& p, size_t& b) {
+        if (b > kScratchKeep) {
+            free(p);
+            p = nullptr;
+            b = 0;
+        }
+    };
+    trim(c->frame_scratch, c->frame_scratch_bytes);
+    trim(c->frame_scratch2, c->frame_scratch2_bytes);
+    trim(c->host_scratch, c->host_scratch_bytes);
+}
+
+// Whether items cover their byte span densely AND in call order, the condition
+// for moving whole spans (DMA, or the flat call's span copy): the span at most
+// twice their bytes plus 1 MiB, and the jumps between consecutive start
+// addresses summing to at most twice the span plus 1 MiB.  Pieces are runs in
+// call order cut at the piece size, so a shuffled batch over a large buffer
+// would cut into pieces of one or two items, each moving a whole span (ADVICE
+// r05).  A scan is kept per part of the batch (pool threads), then merged in
+// part order.
+struct SpanScan {
+    uint64_t lo = ~0ull, hi = 0, sum = 0, jumps = 0;
+    uint64_t first = ~0ull, last = ~0ull;  // the part's first and last start address
+    bool any() const { return first != ~0ull; }
+};
+inline void span_add(SpanScan& s, uint64_t a, uint64_t len) {
+    s.lo = a < s.lo ? a : s.lo;
+    s.hi = a + len > s.hi ? a + len : s.hi;
+    s.sum += len;
+    if (s.last != ~0ull) s.jumps += a > s.last ? a - s.last : s.last - a;
+    if (s.first == ~0ull) s.first = a;
+    s.last = a;
+}
+// parts in call order -> the whole batch's scan (the jump between parts included)
+inline SpanScan span_merge(const SpanScan* p, uint32_t np) {
+    SpanScan t;
+    for (uint32_t j = 0; j < np; ++j) {
+        if (!p[j].any()) continue;
+        if (t.any()) t.jumps += p[j].first > t.last ? p[j].first - t.last : t.last - p[j].first;
+        else t.first = p[j].first;
+        t.lo = p[j].lo < t.lo ? p[j].lo : t.lo;
+        t.hi = p[j].hi > t.hi ? p[j].hi : t.hi;
+        t.sum += p[j].sum;
+        t.jumps += p[j].jumps;
+        t.last = p[j].last;
+    }
+    return t;
+}
+inline bool span_dense(const SpanScan& s) {
+    if (!s.any() || s.hi <= s.lo) return false;
+    const uint64_t span = s.hi - s.lo;
+    return span <= 2 * s.sum + (1ull << 20) && s.jumps <= 2 * span + (1ull << 20);
+}
 
 struct DeviceGuard {
     int prev = -1;
@@ -170,6 +248,28 @@ void parallel_ranges(lvlip_csum_ctx* c, uint64_t n, uint64_t min_per_thread, F f
         return;
     }
     c->pool.run((int)t, [&](int k) { fn(n * (uint64_t)k / t, n * (uint64_t)(k + 1) / t); });
+}
+
+// span_dense over n items (start address addr_of(q), length len_of(q); items
+// of length <= 0 skipped), scanned in parts of at least 4096 items (at most
+// 256 parts) on the pool threads.
+template <class Addr, class Len>
+bool dense_ordered(lvlip_csum_ctx* c, uint32_t n, const Addr& addr_of, const Len& len_of) {
+    constexpr uint32_t kParts = 256;
+    SpanScan part[kParts];
+    const uint32_t np = n / 4096u < 1u ? 1u : (n / 4096u > kParts ? kParts : n / 4096u);
+    parallel_ranges(c, np, 1, [&](uint64_t plo, uint64_t phi) {
+        for (uint64_t j = plo; j < phi; ++j) {
+            SpanScan s;
+            const uint32_t a = (uint32_t)((uint64_t)n * j / np), b = (uint32_t)((uint64_t)n * (j + 1) / np);
+            for (uint32_t q = a; q < b; ++q) {
+                const int64_t l = (int64_t)len_of(q);
+                if (l > 0) span_add(s, (uint64_t)addr_of(q), (uint64_t)l);
+            }
+            part[j] = s;
+        }
+    });
+    return span_dense(span_merge(part, np));
 }
 
 }  // namespace lvlip_ctx

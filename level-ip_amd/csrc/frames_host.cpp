@@ -106,8 +106,9 @@ inline uint32_t frames_per_piece(const lvlip_csum_ctx* c, int mode) {
 // first_piece (LVLIP_FIRST_PIECE, 4 MiB) up to its piece size
 // (LVLIP_PIECE_MAX, 32 MiB).
 inline uint64_t piece_bytes(const lvlip_csum_ctx* c, uint32_t idx) {
-    const uint64_t r = idx < 16 ? c->first_piece << idx : c->piece;
-    return r < c->piece ? r : c->piece;
+    // first_piece <= piece (lvlip_csum_ctx_create), and the shift is taken only
+    // while it stays below piece: no overflow for any LVLIP_FIRST_PIECE
+    return idx < 16 && c->first_piece <= (c->piece >> idx) ? c->first_piece << idx : c->piece;
 }
 
 // LVLIP_FRAME_TRACE=1 (read when the context is made): one line per call on
@@ -128,6 +129,9 @@ thread_local Trace g_trace;
 // array (TX: the host applies that piece's records while later pieces run).
 struct PieceDone {
     virtual void done(uint32_t first, uint32_t k) = 0;
+    // no further piece is worth issuing (TX: a malformed frame was seen, the
+    // call will undo and fail)
+    virtual bool stop() const { return false; }
 };
 
 // drain() plus the piece callback; the slot remembers its piece's range.
@@ -167,6 +171,7 @@ struct FrameSlots {
 int launch_frame_piece(lvlip_csum_ctx* c, Slot& s, int mode, uint64_t bytes, uint32_t k, void* user_out,
                        const uint8_t* src = nullptr, const uint8_t* dev_base = nullptr) {
     hipError_t e;
+    if (const int rc = count_piece(c); rc != LVLIP_OK) return rc;
     const size_t nout = (size_t)k * out_bytes(mode);
     if (bytes <= c->direct_max && (dev_base || !src)) {
         const int rc = lvlip_frames_host_launch(mode, dev_base ? dev_base : s.dh_bytes,
@@ -186,6 +191,7 @@ int launch_frame_piece(lvlip_csum_ctx* c, Slot& s, int mode, uint64_t bytes, uin
         if ((e = hipMemcpyAsync(s.d_bytes, src ? src : s.h_bytes, nb, hipMemcpyHostToDevice, s.stream)) !=
             hipSuccess)
             return fail(c, e, "H2D frames");
+        c->stats.h2d_bytes += nb;
     }
     const int rc = lvlip_frames_host_launch(mode, dev_base ? dev_base : s.d_bytes,
                                             (const lvlip_frame_desc*)s.d_desc, k, s.d_out, s.stream);
@@ -210,6 +216,7 @@ int frames_gather(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode
     while (i < n && rc == LVLIP_OK) {
         Slot& s = c->slot[cur];
         if ((rc = fs.drain_slot(cur)) != LVLIP_OK) break;
+        if (cb && cb->stop()) break;
         lvlip_frame_desc* hd = (lvlip_frame_desc*)s.h_desc;
         const uint32_t first = i;
         const uint64_t pb = piece_bytes(c, idx++);
@@ -279,6 +286,7 @@ int frames_zerocopy(lvlip_csum_ctx* c, const Region& r, const lvlip_frame* fr, u
     while (i < n && rc == LVLIP_OK) {
         Slot& s = c->slot[cur];
         if ((rc = fs.drain_slot(cur)) != LVLIP_OK) break;
+        if (cb && cb->stop()) break;
         lvlip_frame_desc* hd = (lvlip_frame_desc*)s.h_desc;
         const uint32_t first = i;
         const uint64_t pb = piece_bytes(c, idx++);
@@ -314,6 +322,7 @@ int frames_dma(lvlip_csum_ctx* c, const Region& r, const lvlip_frame* fr, uint32
     while (i < n && rc == LVLIP_OK) {
         Slot& s = c->slot[cur];
         if ((rc = fs.drain_slot(cur)) != LVLIP_OK) break;
+        if (cb && cb->stop()) break;
         const uint32_t first = i;
         uintptr_t lo = ~(uintptr_t)0, hi = 0;
         uint32_t k = 0;
@@ -341,14 +350,14 @@ int frames_dma(lvlip_csum_ctx* c, const Region& r, const lvlip_frame* fr, uint32
     return fs.finish(rc, cur);
 }
 
-// The region holding every frame (nullptr if there is none), with what the
-// DMA decision needs of the frames: their byte span [lo, hi), their total
-// length, and whether each one's 16-B span fits the arena.  One pass over the
-// frame array on the pool threads (it precedes the first piece).
+// The region holding every frame (nullptr if there is none), whether the
+// frames cover their span densely and in order (span_dense, ctx_impl.h: the
+// condition for DMA of whole spans), and whether each one's 16-B span fits
+// the arena.  One pass over the frame array on the pool threads (it precedes
+// the first piece).
 struct RegionScan {
     const Region* r = nullptr;
-    uintptr_t lo = ~(uintptr_t)0, hi = 0;
-    uint64_t sum = 0;
+    bool dense = false;
     bool fits = true;
 };
 RegionScan scan_region(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n) {
@@ -357,38 +366,34 @@ RegionScan scan_region(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n) {
     const Region* r = find_region(c, fr[0].head, fr[0].len);
     if (!r) return out;
     constexpr uint32_t kParts = 256;
-    struct Part {
-        uintptr_t lo, hi;
-        uint64_t sum;
-        bool in, fits;
-    } part[kParts];
-    const uint32_t np = n < kParts ? n : kParts;
+    SpanScan part[kParts];
+    bool in[kParts], fits[kParts];
+    // parts of at least 2048 frames (a small call scans on the calling thread)
+    const uint32_t np = n / 2048u < 1u ? 1u : (n / 2048u > kParts ? kParts : n / 2048u);
     const uint8_t *r0 = r->host, *r1 = r->host + r->bytes;
     const uint64_t arena = c->arena;
     parallel_ranges(c, np, 1, [&](uint64_t plo, uint64_t phi) {
         for (uint64_t j = plo; j < phi; ++j) {
-            Part p{~(uintptr_t)0, 0, 0, true, true};
+            SpanScan p;
+            bool pin = true, pfits = true;
             const uint32_t a = (uint32_t)((uint64_t)n * j / np), b = (uint32_t)((uint64_t)n * (j + 1) / np);
             for (uint32_t i = a; i < b; ++i) {
                 const uint8_t* h = (const uint8_t*)fr[i].head;
-                p.in = p.in && h && h >= r0 && h + fr[i].len <= r1;
-                const uintptr_t x = (uintptr_t)h, e = x + fr[i].len;
-                p.lo = x < p.lo ? x : p.lo;
-                p.hi = e > p.hi ? e : p.hi;
-                p.sum += fr[i].len;
-                p.fits = p.fits && align16((uint64_t)fr[i].len + 15u) <= arena;
+                pin = pin && h && h >= r0 && h + fr[i].len <= r1;
+                span_add(p, (uint64_t)(uintptr_t)h, fr[i].len);
+                pfits = pfits && align16((uint64_t)fr[i].len + 15u) <= arena;
             }
             part[j] = p;
+            in[j] = pin;
+            fits[j] = pfits;
         }
     });
     for (uint32_t j = 0; j < np; ++j) {
-        if (!part[j].in) return RegionScan{};
-        out.lo = part[j].lo < out.lo ? part[j].lo : out.lo;
-        out.hi = part[j].hi > out.hi ? part[j].hi : out.hi;
-        out.sum += part[j].sum;
-        out.fits = out.fits && part[j].fits;
+        if (!in[j]) return RegionScan{};
+        out.fits = out.fits && fits[j];
     }
     out.r = r;
+    out.dense = out.fits && span_dense(span_merge(part, np));
     return out;
 }
 
@@ -397,9 +402,10 @@ RegionScan scan_region(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n) {
 int frames_run_(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, uint8_t* out,
                 PieceDone* cb) {
     DeviceGuard g(c->device);
+    begin_gpu_call(c);
     const RegionScan rs = scan_region(c, fr, n);
     if (const Region* r = rs.r) {
-        const bool dense = rs.fits && rs.hi - rs.lo <= 2 * rs.sum + (1ull << 20);
+        const bool dense = rs.dense;
         // a zero-copy region is read in place, unless the frames lie densely
         // in it and the call sums whole frames: then the copy engine moves
         // the spans, as for a DMA region (the region is pinned and mapped
@@ -413,8 +419,8 @@ int frames_run_(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n, int mode, 
         // needs 74 B of each ~800-B frame: those are gathered (mixed frames,
         // 512K: 7.0-7.3 GB/s of headers gathered, 3.2-3.4 read in place,
         // 1.2 as DMA'd spans)
-        // DMA only when the frames lie densely in the region (a slab of
-        // frames): the spans are copied whole, gaps included
+        // DMA only when the frames lie densely and in order in the region (a
+        // slab of frames): the spans are copied whole, gaps included
         if (mode != M_RX && dense) return frames_dma(c, *r, fr, n, mode, out, cb);
     }
     // scattered: every frame's slot offset (a prefix sum over the frames'
@@ -497,6 +503,7 @@ struct TxApply final : PieceDone {
     uint32_t* undo;
     bool bad = false;
     TxApply(lvlip_csum_ctx* c_, lvlip_frame* f, uint64_t* r, uint32_t* u) : c(c_), fr(f), rec(r), undo(u) {}
+    bool stop() const override { return bad; }
     void done(uint32_t first, uint32_t k) override {
         if (bad) return;
         for (uint32_t i = first; i < first + k; ++i)
@@ -526,10 +533,13 @@ struct TxApply final : PieceDone {
             }
         });
     }
-    // the frames written so far back to their old bytes (the L4 field first:
-    // it may overlap nothing else, but restore in reverse order of writing)
+    // the frames written so far back to their old bytes, in reverse order of
+    // writing (the pieces were applied in index order; within a frame the L4
+    // field was written after the header's)
     void undo_all(uint32_t n) {
-        for (uint32_t q = 0; q < n; ++q) {
+        // last written first: a frame listed twice (in two pieces) gets back
+        // the bytes its first entry saved, the ones from before the call
+        for (uint32_t q = n; q-- > 0;) {
             if (!(rec[q] & kApplied)) continue;
             uint8_t* h = fr[q].head;
             const uint32_t o = (uint32_t)(rec[q] >> 32) & 0xffu;
@@ -540,6 +550,21 @@ struct TxApply final : PieceDone {
     }
 };
 
+// Whether a frame is longer than the context's arena (the frame calls'
+// LVLIP_ERANGE, on every path and on both sides of cpu_max).
+bool first_too_long(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n) {
+    std::atomic<bool> big{false};
+    const uint64_t arena = c->arena;
+    parallel_ranges(c, n, 65536, [&big, fr, arena](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; ++i)
+            if (fr[i].len > arena) {
+                big.store(true, std::memory_order_relaxed);
+                return;
+            }
+    });
+    return big.load(std::memory_order_relaxed);
+}
+
 }  // namespace
 
 extern "C" {
@@ -549,12 +574,32 @@ int lvlip_rx_verify(lvlip_csum_ctx* ctx, const lvlip_frame* frames, uint32_t n, 
     // two checksums per frame at most: n as the _dev call
     if (!ctx || (n && (!frames || !verdict)) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
-    return frames_run(ctx, frames, n, (flags & LVLIP_RX_VERIFY_L4) ? M_RX_L4 : M_RX, verdict);
+    const int mode = (flags & LVLIP_RX_VERIFY_L4) ? M_RX_L4 : M_RX;
+    // a frame longer than the arena: LVLIP_ERANGE on every path (the header-
+    // only call moves at most kHdrWin <= 4096 B of a frame and never refuses)
+    if (mode == M_RX_L4 && first_too_long(ctx, frames, n)) return LVLIP_ERANGE;
+    if (n <= ctx->cpu_max) {  // the calling thread (lvlip_csum_ctx_set_cpu_max)
+        ctx->stats.cpu_calls++;
+        return lvlip_rx_verify_cpu(frames, n, flags, verdict);
+    }
+    const int rc = frames_run(ctx, frames, n, mode, verdict);
+    trim_scratch(ctx);
+    return rc;
 }
 
 int lvlip_tx_checksum(lvlip_csum_ctx* ctx, lvlip_frame* frames, uint32_t n) {
     if (!ctx || (n && !frames) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
+    if (n <= ctx->cpu_max) {
+        // the calling thread (lvlip_csum_ctx_set_cpu_max), with the GPU
+        // path's checks in its order: a NULL or short frame, then a frame
+        // longer than the arena, then a malformed one (the CPU call)
+        for (uint32_t i = 0; i < n; ++i)
+            if (!frames[i].head || frames[i].len < kEth + 20u) return LVLIP_EINVAL;
+        if (first_too_long(ctx, frames, n)) return LVLIP_ERANGE;
+        ctx->stats.cpu_calls++;
+        return lvlip_tx_checksum_cpu(frames, n);
+    }
     // the context's scratch: n records, then n undo words
     uint64_t* rec = (uint64_t*)scratch(ctx, 12 * (size_t)n);
     if (!rec) return LVLIP_ENOMEM;
@@ -572,10 +617,12 @@ int lvlip_tx_checksum(lvlip_csum_ctx* ctx, lvlip_frame* frames, uint32_t n) {
         if (b) bad.store(true, std::memory_order_relaxed);
     });
     if (bad.load(std::memory_order_relaxed)) return LVLIP_EINVAL;
+    if (first_too_long(ctx, frames, n)) return LVLIP_ERANGE;
     TxApply ap(ctx, frames, rec, undo);
     int rc = frames_run(ctx, frames, n, M_TX, (uint8_t*)rec, &ap);
     if (rc == LVLIP_OK && ap.bad) rc = LVLIP_EINVAL;
     if (rc != LVLIP_OK) ap.undo_all(n);  // a malformed frame (or a failure): every frame as it was
+    trim_scratch(ctx);
     return rc;
 }
 

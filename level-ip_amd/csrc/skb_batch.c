@@ -198,6 +198,89 @@ void lvlip_tx_apply(uint32_t m, uint8_t *const *field, const uint16_t *csum)
     for (uint32_t k = 0; k < m; k++) memcpy(field[k], &csum[k], 2); /* raw store */
 }
 
+/* ------------------------------------------- f1/f2 on the calling thread (CPU) */
+
+/* One frame's RX verdict, the decisions of rx_plan_range in ip_rcv's order
+ * (src/ip_input.c:17-60) with the checksums computed at once: a failing header
+ * checksum (src/ip_input.c:38-43) outranks every verdict decided after it
+ * (unknown protocol, short L4), as lvlip_rx_apply resolves the pending ones. */
+static uint8_t rx_verdict_one(const uint8_t *h, uint32_t flen, uint32_t flags)
+{
+    if (!h || flen < ETH_HDR_LEN + 20u) return LVLIP_RX_SHORT;
+    if (be16(h + 12) != ETH_P_IP) return LVLIP_RX_NOT_IP; /* src/netdev.c:67-80 */
+    const uint8_t *ih = h + ETH_HDR_LEN;
+    const uint32_t ihl = ih[0] & 0x0fu;
+    if ((ih[0] >> 4) != 4u) return LVLIP_RX_BAD_VERSION; /* src/ip_input.c:22 */
+    if (ihl < 5u) return LVLIP_RX_BAD_IHL;                /* src/ip_input.c:27 */
+    if (ih[8] == 0u) return LVLIP_RX_TTL0;                /* src/ip_input.c:32 */
+    if (flen < ETH_HDR_LEN + ihl * 4u) return LVLIP_RX_SHORT;
+    if (checksum((void *)ih, (int)(ihl * 4u), 0) != 0) return LVLIP_RX_BAD_CSUM; /* :38-43 */
+    const uint32_t proto = ih[9];
+    if (proto != PROTO_TCP && proto != PROTO_ICMP) return LVLIP_RX_UNKNOWN_PROTO; /* :51-60 */
+    if (flags & LVLIP_RX_VERIFY_L4) {
+        const uint32_t iplen = be16(ih + 2);
+        if (iplen < ihl * 4u || flen < ETH_HDR_LEN + iplen) return LVLIP_RX_SHORT;
+        const uint32_t l4len = iplen - ihl * 4u;
+        const uint32_t seed = proto == PROTO_TCP ? lvlip_pseudo_sum_rfc(le32(ih + 12), le32(ih + 16), PROTO_TCP,
+                                                                         (uint16_t)l4len)
+                                                 : 0u;
+        if (checksum((void *)(ih + ihl * 4u), (int)l4len, (int)seed) != 0) return LVLIP_RX_BAD_L4;
+    }
+    return LVLIP_RX_OK;
+}
+
+int lvlip_rx_verify_cpu(const lvlip_frame *frames, uint32_t n, uint32_t flags, uint8_t *verdict)
+{
+    if ((n && (!frames || !verdict)) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
+    for (uint32_t i = 0; i < n; i++) {
+        pf_header(frames, i, n);
+        verdict[i] = rx_verdict_one(frames[i].head, frames[i].len, flags);
+    }
+    return LVLIP_OK;
+}
+
+/* tx_plan_range's refusal, for one frame (0 = well formed) */
+static int tx_malformed(const lvlip_frame *f)
+{
+    const uint8_t *h = f->head;
+    if (!h || f->len < ETH_HDR_LEN + 20u) return 1;
+    const uint8_t *ih = h + ETH_HDR_LEN;
+    const uint32_t ihl = ih[0] & 0x0fu, iplen = be16(ih + 2);
+    return (ih[0] >> 4) != 4u || ihl < 5u || iplen < ihl * 4u || f->len < ETH_HDR_LEN + iplen;
+}
+
+int lvlip_tx_checksum_cpu(lvlip_frame *frames, uint32_t n)
+{
+    if ((n && !frames) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
+    /* every frame checked before the first store: a malformed one leaves the
+     * batch untouched, as the GPU call does */
+    for (uint32_t i = 0; i < n; i++) {
+        pf_header(frames, i, n);
+        if (tx_malformed(&frames[i])) return LVLIP_EINVAL;
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        pf_header(frames, i, n);
+        uint8_t *ih = frames[i].head + ETH_HDR_LEN;
+        const uint32_t ihl = ih[0] & 0x0fu, l4len = be16(ih + 2) - ihl * 4u, proto = ih[9];
+        uint8_t *l4 = ih + ihl * 4u;
+        /* each field's current u16 taken out of the seed (tx_plan_range): the
+         * reference's zero-then-sum, src/tcp_output.c:110,126, src/icmpv4.c:46-47 */
+        if (proto == PROTO_TCP && l4len >= 20u) {
+            const uint32_t seed = lvlip_pseudo_sum(le32(ih + 12), le32(ih + 16), PROTO_TCP, (uint16_t)l4len) -
+                                  le16(l4 + 16);
+            const uint16_t c = checksum(l4, (int)l4len, (int)seed);
+            memcpy(l4 + 16, &c, 2);
+        } else if (proto == PROTO_ICMP && l4len >= 4u) {
+            const uint16_t c = checksum(l4, (int)l4len, (int)(0u - le16(l4 + 2)));
+            memcpy(l4 + 2, &c, 2);
+        }
+        /* src/ip_output.c:42,53 (the header sum does not cover the L4 bytes) */
+        const uint16_t hc = checksum(ih, (int)(ihl * 4u), (int)(0u - le16(ih + 10)));
+        memcpy(ih + 10, &hc, 2);
+    }
+    return LVLIP_OK;
+}
+
 /* ----------------------------------------------------------------- f4: RFC 1624 */
 
 /* One's-complement add of two 16-bit values (end-around carry). */
@@ -348,6 +431,32 @@ int lvlip_tx_checksum_skb_list(lvlip_csum_ctx *ctx, struct sk_buff_head *q)
     const int64_t n = skb_list_frames(q, 0, &f);
     if (n < 0) return LVLIP_EINVAL;
     const int rc = n ? lvlip_tx_checksum(ctx, f, (uint32_t)n) : LVLIP_OK;
+    free(f);
+    return rc == LVLIP_OK ? (int)n : rc;
+}
+
+int lvlip_rx_verify_skb_list_cpu(struct sk_buff_head *q, uint32_t flags, uint8_t *verdict, uint32_t cap)
+{
+    if (!q) return LVLIP_EINVAL;
+    lvlip_frame *f = NULL;
+    const int64_t n = skb_list_frames(q, 1, &f);
+    if (n < 0) return LVLIP_EINVAL;
+    if ((uint64_t)n > cap) {
+        free(f);
+        return LVLIP_ERANGE;
+    }
+    const int rc = n ? lvlip_rx_verify_cpu(f, (uint32_t)n, flags, verdict) : LVLIP_OK;
+    free(f);
+    return rc == LVLIP_OK ? (int)n : rc;
+}
+
+int lvlip_tx_checksum_skb_list_cpu(struct sk_buff_head *q)
+{
+    if (!q) return LVLIP_EINVAL;
+    lvlip_frame *f = NULL;
+    const int64_t n = skb_list_frames(q, 0, &f);
+    if (n < 0) return LVLIP_EINVAL;
+    const int rc = n ? lvlip_tx_checksum_cpu(f, (uint32_t)n) : LVLIP_OK;
     free(f);
     return rc == LVLIP_OK ? (int)n : rc;
 }

@@ -81,6 +81,19 @@ class Frame(ctypes.Structure):  # include/lvlip_skb.h: lvlip_frame
     _fields_ = [("head", ctypes.c_void_p), ("len", ctypes.c_uint32)]
 
 
+class CtxStats(ctypes.Structure):  # include/lvlip_csum.h: lvlip_ctx_stats
+    _fields_ = [("gpu_calls", ctypes.c_uint64), ("cpu_calls", ctypes.c_uint64),
+                ("pieces", ctypes.c_uint64), ("h2d_bytes", ctypes.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+# include/lvlip_csum.h: host calls of at most this many packets / frames run on
+# the calling thread unless the context says otherwise (LVLIP_CPU_MAX)
+CPU_MAX_DEFAULT = 2048
+
+
 # RX verdicts and flags (include/lvlip_skb.h)
 RX_OK, RX_NOT_IP, RX_SHORT, RX_BAD_VERSION, RX_BAD_IHL, RX_TTL0, RX_BAD_CSUM, RX_BAD_L4, \
     RX_UNKNOWN_PROTO = range(1, 10)
@@ -219,6 +232,16 @@ SIGNATURES = {
     "lvlip_rx_verify_skb_list": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                 ctypes.c_void_p, ctypes.c_uint32]),
     "lvlip_tx_checksum_skb_list": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    # round 6: size-based dispatch, counters, context-free CPU frame calls
+    "lvlip_csum_ctx_set_cpu_max": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    "lvlip_csum_ctx_cpu_max": (ctypes.c_uint32, [ctypes.c_void_p]),
+    "lvlip_csum_ctx_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CtxStats)]),
+    "lvlip_rx_verify_cpu": (ctypes.c_int, [ctypes.POINTER(Frame), ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_void_p]),
+    "lvlip_tx_checksum_cpu": (ctypes.c_int, [ctypes.POINTER(Frame), ctypes.c_uint32]),
+    "lvlip_rx_verify_skb_list_cpu": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                                    ctypes.c_uint32]),
+    "lvlip_tx_checksum_skb_list_cpu": (ctypes.c_int, [ctypes.c_void_p]),
     "lvlip_auto_kernel": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint32, ctypes.POINTER(LaunchCfg)]),
     "lvlip_batch_launches": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.POINTER(LaunchCfg)]),
     "lvlip_build_id": (ctypes.c_char_p, []),
@@ -579,6 +602,23 @@ def icmp_echo_reply_fill(frames) -> int:
     return r
 
 
+def rx_verify_cpu(frames, flags: int = 0) -> np.ndarray:
+    """lvlip_rx_verify_cpu: the RX verdicts on the calling thread (no context)."""
+    n = len(frames)
+    arr, keep = frames_array(frames)
+    verdict = np.zeros(max(n, 1), dtype=np.uint8)
+    _check(_lib.lvlip_rx_verify_cpu(arr, n, flags, verdict.ctypes.data), "lvlip_rx_verify_cpu")
+    del keep
+    return verdict[:n]
+
+
+def tx_checksum_cpu(frames) -> None:
+    """lvlip_tx_checksum_cpu: the TX fill on the calling thread (no context)."""
+    arr, keep = frames_array(frames)
+    _check(_lib.lvlip_tx_checksum_cpu(arr, len(frames)), "lvlip_tx_checksum_cpu")
+    del keep
+
+
 def tx_apply(field: np.ndarray, csum: np.ndarray) -> None:
     f = np.ascontiguousarray(field, dtype=np.uint64)
     c = np.ascontiguousarray(csum, dtype=np.uint16)
@@ -588,12 +628,31 @@ def tx_apply(field: np.ndarray, csum: np.ndarray) -> None:
 # ------------------------------------------------------------ host batches --
 
 class Context:
-    """lvlip_csum_ctx: pinned arena + device arena + streams, one thread at a time."""
+    """lvlip_csum_ctx: pinned arena + device arena + streams, one thread at a time.
 
-    def __init__(self, device: int = 0, arena_bytes: int = 0):
+    cpu_max: host calls of at most this many packets / frames run on the
+    calling thread with the library's CPU code (lvlip_csum_ctx_set_cpu_max);
+    None keeps the library's default (LVLIP_CPU_MAX, else CPU_MAX_DEFAULT), 0
+    sends every call to the GPU."""
+
+    def __init__(self, device: int = 0, arena_bytes: int = 0, cpu_max: Optional[int] = None):
         self._h = ctypes.c_void_p()
         _check(_lib.lvlip_csum_ctx_create(ctypes.byref(self._h), device, arena_bytes),
                "lvlip_csum_ctx_create")
+        if cpu_max is not None:
+            self.set_cpu_max(cpu_max)
+
+    def set_cpu_max(self, cpu_max: int) -> None:
+        _check(_lib.lvlip_csum_ctx_set_cpu_max(self._h, int(cpu_max)), "lvlip_csum_ctx_set_cpu_max")
+
+    @property
+    def cpu_max(self) -> int:
+        return int(_lib.lvlip_csum_ctx_cpu_max(self._h))
+
+    def stats(self) -> dict:
+        st = CtxStats()
+        _check(_lib.lvlip_csum_ctx_stats(self._h, ctypes.byref(st)), "lvlip_csum_ctx_stats")
+        return st.as_dict()
 
     def close(self) -> None:
         if self._h:

@@ -23,10 +23,13 @@
  * src/tcp_output.c:177,264,495, src/icmpv4.c:53; a retransmit queue keeps it)
  * and links the copy into one sk_buff_head, as skb_queue_tail links skbs
  * (include/skbuff.h:55-59).  A flush then fills every queued frame's fields in
- * ONE call, lvlip_tx_checksum_skb_list on the GPU (include/lvlip_skb.h), or
- * lets the caller fill them (the CPU variant of the test: the oracle's
- * tx_fill on lvlip_txq_frames' frames), and hands each skb in queue order to
- * the real dst_neigh_output (src/dst.c:6-30 -> netdev_transmit -> tun_write).
+ * ONE call (lvlip_txq_fill: lvlip_tx_checksum_skb_list through a context,
+ * which runs a small queue on this thread and a large one on the GPU,
+ * include/lvlip_skb.h; with the CPU fill when the GPU call cannot run or
+ * fails), or lets the caller fill them (the CPU variant of the test: the
+ * oracle's tx_fill on lvlip_txq_frames' frames), and hands each skb in queue
+ * order to the real dst_neigh_output (src/dst.c:6-30 -> netdev_transmit ->
+ * tun_write).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -89,6 +92,9 @@ int lvlip_txq_output(struct sk_buff *skb)
 
 int lvlip_txq_len(void) { return (int)g_txq.qlen; }
 
+/* the queue itself (an sk_buff_head), for a caller that makes the batch call directly */
+struct sk_buff_head *lvlip_txq_queue(void) { return (struct sk_buff_head *)&g_txq; }
+
 /* checksum computations the TX path deferred since the last call */
 unsigned long lvlip_txq_deferred(void)
 {
@@ -114,11 +120,73 @@ int lvlip_txq_frames(lvlip_frame *out, int cap)
     return k;
 }
 
-/* The batch step: every queued frame's checksums in one GPU call.  Returns
- * the number of frames, or LVLIP_E*. */
-int lvlip_txq_fill_gpu(lvlip_csum_ctx *ctx)
+/* A frame queued as if ip_output had queued it (the tests' malformed frame):
+ * len bytes from its Ethernet header, route and device taken from the last
+ * queued skb.  Returns 0, or -1 (out of memory, or nothing queued yet). */
+int lvlip_txq_inject(const uint8_t *frame, unsigned int len)
 {
-    return lvlip_tx_checksum_skb_list(ctx, (struct sk_buff_head *)&g_txq);
+    if (!g_txq.qlen || len < ETH_LEN) return -1;
+    struct sk_buff *last = list_entry(g_txq.head.prev, struct sk_buff, list);
+    struct sk_buff *c = alloc_skb(len);
+    if (!c) return -1;
+    memcpy(c->head, frame, len);
+    c->data = c->head + ETH_LEN;
+    c->len = len - ETH_LEN;
+    c->dev = last->dev;
+    c->rt = last->rt;
+    skb_queue_tail(&g_txq, c);
+    return 0;
+}
+
+/* What a flush did (lvlip_txq_fill). */
+struct lvlip_txq_report {
+    int frames;  /* frames filled */
+    int rc;      /* the batch call's return: frames, or LVLIP_E* (LVLIP_ENODEV: no context) */
+    int cpu;     /* 1 if the fill fell back to this thread's CPU code after a failure */
+    int dropped; /* malformed frames unlinked and freed, never sent */
+};
+
+/* The flush's fill, as INTEGRATION.md §2a gives it to a maintainer: every
+ * queued frame's checksums in ONE call through the context (a queue of at
+ * most the context's cpu_max frames is summed on this thread by the library,
+ * a longer one on the GPU).  No frame may leave with a deferred (zero) field
+ * (src/ip_output.c:53-55 sends whatever the fields hold), so:
+ *   - no context (it could not be made), or the call failed without touching
+ *     the frames for a device / HIP / memory / arena reason: the same fill on
+ *     this thread (lvlip_tx_checksum_skb_list_cpu);
+ *   - LVLIP_EINVAL (a malformed frame: the call left EVERY frame untouched):
+ *     each frame filled on its own on this thread; a frame the fill refuses
+ *     (and one whose skb has no room for the Ethernet header) is unlinked,
+ *     freed and counted, never sent.
+ * Returns the number of frames filled, or a negative LVLIP_E* if even the
+ * CPU fill could not run. */
+int lvlip_txq_fill(lvlip_csum_ctx *ctx, struct lvlip_txq_report *r)
+{
+    struct sk_buff_head *q = (struct sk_buff_head *)&g_txq;
+    memset(r, 0, sizeof *r);
+    int rc = ctx ? lvlip_tx_checksum_skb_list(ctx, q) : LVLIP_ENODEV;
+    r->rc = rc;
+    if (rc >= 0) return r->frames = rc;
+    r->cpu = 1;
+    if (rc != LVLIP_EINVAL) {
+        rc = lvlip_tx_checksum_skb_list_cpu(q);
+        if (rc >= 0) return r->frames = rc;
+        if (rc != LVLIP_EINVAL) return rc;
+    }
+    struct list_head *p, *t;
+    list_for_each_safe(p, t, &g_txq.head) {
+        struct sk_buff *s = list_entry(p, struct sk_buff, list);
+        lvlip_frame f = {s->data - ETH_LEN, s->len + ETH_LEN};
+        if (!s->data || s->data - s->head < ETH_LEN || lvlip_tx_checksum_cpu(&f, 1) != LVLIP_OK) {
+            list_del(&s->list);
+            g_txq.qlen--;
+            free_skb(s);
+            r->dropped++;
+        } else {
+            r->frames++;
+        }
+    }
+    return r->frames;
 }
 
 /* The dispatch step: each queued skb in order to the real dst_neigh_output,

@@ -1,0 +1,81 @@
+"""Times level-ip's own stack per burst / flush, batched and unbatched
+(VERDICT r05 Next #3): where batch-and-dispatch makes level-ip cheaper.
+
+  RX + replies  tests/ref_scale_child.py in time mode: bursts of n echo
+                requests (n = 8 .. 32 768, 64-1 400 B payloads, all answered)
+                through libref_rxq.so (level-ip as it is) and libref_rxtxq.so
+                (one RX verify, the dispatch, one TX flush) with the library's
+                default threshold and with threshold 0 (always the GPU)
+  TX            tests/ref_tx_batch_child.py in time mode: one tcp_send of
+                W bytes (smss 536) sent by tcp_send_next, then the flush,
+                for W = 4 KiB .. 8 MiB, unbatched and batched (both thresholds)
+
+The tap is /dev/null; each figure is the best of 3 after an untimed run of
+the same size (RX), or one run per process (TX).  Prints one JSON object.
+
+    python scripts/compose_timing.py > gpurun_out/r06_compose.json
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "oracle", "_ref")
+BURSTS = [8, 64, 512, 4096, 32768]
+WRITES = [4 << 10, 64 << 10, 1 << 20, 8 << 20]
+
+
+def env_for(cpu_max):
+    env = {k: v for k, v in os.environ.items() if k != "LVLIP_CPU_MAX"}
+    if cpu_max is not None:
+        env["LVLIP_CPU_MAX"] = str(cpu_max)
+    return env
+
+
+def rx(lib, mode, cpu_max=None):
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "o.json")
+        subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ref_scale_child.py"), out,
+                        os.path.join(REF, lib), mode, json.dumps({"time": BURSTS, "kinds": "ok", "seed": 3})],
+                       check=True, stdin=subprocess.DEVNULL, env=env_for(cpu_max), timeout=900)
+        with open(out) as f:
+            return json.load(f)["time"]
+
+
+def tx(lib, mode, w, cpu_max=None):
+    with tempfile.TemporaryDirectory() as d:
+        req, out = os.path.join(d, "r.json"), os.path.join(d, "o.json")
+        with open(req, "w") as f:
+            json.dump([], f)
+        subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ref_tx_batch_child.py"), req, out,
+                        os.path.join(REF, lib), mode, json.dumps({"write_bytes": w, "send_next": 0, "time": True})],
+                       check=True, stdin=subprocess.DEVNULL, env=env_for(cpu_max), timeout=900)
+        with open(out) as f:
+            o = json.load(f)
+        r = {"wall_us": round(o["time"]["tcp_wall_s"] * 1e6, 1), "cpu_us": round(o["time"]["tcp_cpu_s"] * 1e6, 1),
+             "frames": (w + 535) // 536 + 4}
+        if o.get("reports"):
+            r["flush"] = o["reports"][0]
+        return r
+
+
+def main():
+    res = {"rx_bursts": BURSTS, "rx": {}, "tx_writes": WRITES, "tx": {}}
+    res["rx"]["unbatched"] = rx("libref_rxq.so", "unbatched")
+    print("rx unbatched", res["rx"]["unbatched"], file=sys.stderr, flush=True)
+    for tag, cm in (("batched_default", None), ("batched_gpu", 0), ("batched_cpu", 1 << 30)):
+        res["rx"][tag] = rx("libref_rxtxq.so", "batched", cm)
+        print("rx", tag, res["rx"][tag], file=sys.stderr, flush=True)
+    for tag, lib, mode, cm in (("unbatched", "libref_fixclock.so", "unbatched", None),
+                               ("batched_default", "libref_txq.so", "gpu", None),
+                               ("batched_gpu", "libref_txq.so", "gpu", 0),
+                               ("batched_cpu", "libref_txq.so", "gpu", 1 << 30)):
+        res["tx"][tag] = {str(w): tx(lib, mode, w, cm) for w in WRITES}
+        print("tx", tag, res["tx"][tag], file=sys.stderr, flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

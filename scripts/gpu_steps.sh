@@ -12,17 +12,13 @@
 #   bench[:WL]            the default bench line (WL: tcp1500 | tcp9000 | mixed)
 #   e2e[:WL]              the bench line with its host-resident (PCIe-inclusive) rates and small-batch latency
 #   frames                the mixed bench line with its device frame-call diag (TX fill, RX verify)
-#   txstore               scripts/lab_tx_store.py (TX field-store A/B + probes)
-#   fhost[:R]             scripts/lab_frames_host.py (host frame pipeline: ramps, threads; R rounds)
+#   crossover             bench.py --crossover: host calls at n = 1..256K on both sides of the CPU/GPU threshold
+#   compose               scripts/compose_timing.py: level-ip's own stack per burst / flush, batched and not
+#   dispatch              the round-6 dispatch, failure and composition GPU tests alone
 #   rehearse:N            bench.py --gpus N self-launched over gloo, the ranks sharing the one GPU
 #   rehearse_strong:N     the same with --workload tcp1500x64m (64M packets split over the N ranks)
 #   rehearse_root:N       the same with --origin root (the batch scattered from rank 0's GPU first)
-#   wb                    scripts/lab_wb.py (field-store forms paired with the RX + L4 sweep)
-#   txpmc                 FETCH_SIZE / WRITE_SIZE passes of the TX variants
-#   modes:K               K processes of scripts/lab_modes.py (mixed line modes)
 #   numa                  scripts/lab_numa.py (XCD <-> address-class locality probe)
-#   cputh, cputh_spin     scripts/lab_cpu_threads.py (host CPU time of the frame calls per thread;
-#                         _spin: LVLIP_BLOCK_MIN=0)
 #   window:SET            scripts/lab_window.py with LAB_SET=SET (read-order probes)
 #   evidence:WL           scripts/evidence.sh for WL (bench + trace + PMC of the kernel AUTO runs)
 #   pmc:WL                the PMC passes of that evidence alone (scripts/profile.sh)
@@ -32,7 +28,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 
 run() {  # name, seconds, command...
   local name=$1 secs=$2; shift 2
@@ -56,26 +52,12 @@ for step in "$@"; do
     rehearse:*) n=${step#rehearse:}; run "rehearse_n$n" 300 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --steps 50 --warmup 10 ;;
     rehearse_strong:*) n=${step#rehearse_strong:}; run "rehearse_strong_n$n" 400 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --workload tcp1500x64m --steps 20 --warmup 5 ;;
     rehearse_root:*) n=${step#rehearse_root:}; run "rehearse_root_n$n" 300 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --origin root --steps 50 --warmup 10 ;;
-    wb) run wb 400 python scripts/lab_wb.py "gpurun_out/${TAG}_wb.json" 5 ;;
-    fhost) run fhost 500 python scripts/lab_frames_host.py "gpurun_out/${TAG}_frames_host.json" 3 ;;
-    fhost:*) r=${step#fhost:}; run fhost 500 python scripts/lab_frames_host.py "gpurun_out/${TAG}_frames_host.json" "$r" ;;
-    txstore) run txstore 400 python scripts/lab_tx_store.py "gpurun_out/${TAG}_tx_store.json" 7 ;;
-    txpmc)
-      for v in ${TXPMC_VARIANTS:-tx_product tx_nt tx_sec32 rx_l4}; do
-        for c in FETCH_SIZE WRITE_SIZE; do
-          run "txpmc_${v}_$c" 180 /opt/rocm/bin/rocprofv3 --pmc "$c" --kernel-include-regex "k_flat2|k_probe" \
-            --output-format csv -d "gpurun_out/txpmc/${v}_$c" -o "${v}_$c" -- python3 scripts/lab_tx_store.py --only "$v" 20
-        done
-      done
-      run txtrace 180 /opt/rocm/bin/rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/txpmc/trace \
-        -o trace -- python3 scripts/lab_tx_store.py --only tx_product 20 ;;
+    crossover) run crossover 600 python bench.py --crossover --steps 5 --warmup 2 --no-cpu-baseline ;;
+    compose) run compose 900 sh -c "python scripts/compose_timing.py > gpurun_out/${TAG}_compose.json" ;;
+    dispatch) run dispatch 900 python -u -m pytest tests/test_dispatch_gpu.py tests/test_ref_tx_batch.py \
+                tests/test_ref_rx_batch.py tests/test_ref_scale.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     numa) run numa 300 python scripts/lab_numa.py "gpurun_out/${TAG}_numa.json" ;;
-    cputh) run cputh 300 python scripts/lab_cpu_threads.py "gpurun_out/${TAG}_cpu_threads.json" 40 ;;
-    cputh_spin) run cputh_spin 300 env LVLIP_BLOCK_MIN=0 python scripts/lab_cpu_threads.py "gpurun_out/${TAG}_cpu_threads_spin.json" 40 ;;
     window:*) set_=${step#window:}; run "window_$set_" 400 env LAB_SET="$set_" python scripts/lab_window.py "gpurun_out/${TAG}_window_$set_.json" ;;
-    modes:*)
-      k=${step#modes:}
-      for i in $(seq 1 "$k"); do run "modes_p$i" 240 python scripts/lab_modes.py "gpurun_out/${TAG}_modes_p$i.json"; done ;;
     evidence:*|pmc:*)
       wl=${step#*:}
       case "$wl" in mixed) kre=k_flat2 ;; *) kre=k_window ;; esac  # the kernel AUTO runs (bench.py KERNEL_FN)

@@ -12,6 +12,13 @@ for p in (PKG, ORACLE, ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# A context's host calls of at most cpu_max packets / frames run on the CPU
+# (include/lvlip_csum.h, lvlip_csum_ctx_set_cpu_max).  The parity tests are
+# about the GPU path, so their contexts send every call to the GPU; the
+# dispatch tests (test_dispatch_gpu.py, test_ref_*_batch.py) set the
+# threshold, or remove this, explicitly.
+os.environ.setdefault("LVLIP_CPU_MAX", "0")
+
 def _may_rebuild() -> bool:
     """Whether a stale library is rebuilt here or stops the run.
     LVLIP_REBUILD=1 / 0 decides explicitly; by default a machine without a GPU

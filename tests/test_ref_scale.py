@@ -1,0 +1,80 @@
+"""Both batch-and-dispatch steps at scale on level-ip's own stack (VERDICT r05
+Next #3): an RX burst of tens of thousands of echo requests of every ip_rcv
+kind, through level-ip as it is (oracle/_ref/libref_rxq.so, one skb at a time,
+every checksum on the CPU) and through the batched stack
+(oracle/_ref/libref_rxtxq.so: one lvlip_rx_verify_skb_list over the queue, the
+dispatch, ip_rcv's header sum answered by the verdict, the replies' checksums
+deferred and filled by one flush).  The frames on the tap must be identical,
+reply for reply (tests/ref_scale_child.py).  Skipped when oracle/_ref was not
+built (it needs /root/reference at build time)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "oracle", "_ref")
+RXQ = os.path.join(REF, "libref_rxq.so")
+RXTXQ = os.path.join(REF, "libref_rxtxq.so")
+CHILD = os.path.join(ROOT, "tests", "ref_scale_child.py")
+
+pytestmark = pytest.mark.skipif(not (os.path.exists(RXQ) and os.path.exists(RXTXQ)),
+                                reason="oracle/_ref/libref_{rxq,rxtxq}.so not built")
+
+
+def run(tmp_path, lib, mode, opts, cpu_max=None, tag=None):
+    env = {k: v for k, v in os.environ.items() if k != "LVLIP_CPU_MAX"}
+    if cpu_max is not None:
+        env["LVLIP_CPU_MAX"] = str(cpu_max)
+    out = tmp_path / f"{tag or mode}.json"
+    r = subprocess.run([sys.executable, CHILD, str(out), lib, mode, json.dumps(opts)], stdin=subprocess.DEVNULL,
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(out.read_text())
+
+
+def _check(base, got, n):
+    assert got["frames"] == base["frames"]
+    # the ARP reply and one echo reply per answered request
+    assert len(base["frames"]) > n // 4
+    # unbatched: ip_rcv sums every header that reaches :38; batched: none
+    assert base["cpu_header_sums"] > 0 and base["batch_header_sums"] == 0
+    assert got["cpu_header_sums"] == 0 and got["batch_header_sums"] == got["verdicts"].get("1", 0)
+
+
+def test_rx_tx_burst_oracle_composition(tmp_path):
+    """CPU: 2 000 frames with the oracle's verdicts and TX fill in place of the
+    library (the harness's own check on a machine without a GPU)."""
+    opts = {"n": 2000, "seed": 5, "kinds": "all"}
+    base = run(tmp_path, RXQ, "unbatched", opts)
+    _check(base, run(tmp_path, RXTXQ, "oracle", opts), 2000)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cpu_max", [None, 0])
+def test_rx_tx_burst_at_scale(tmp_path, cpu_max):
+    """30 000 frames of every kind, one RX call and one TX flush: the default
+    threshold and threshold 0 both put these calls on the GPU (30 000 frames
+    and ~11 000 replies are above the default); the tap bytes equal the
+    unbatched stack's, frame for frame, and no header is summed on the CPU."""
+    opts = {"n": 30000, "seed": 6, "kinds": "all"}
+    base = run(tmp_path, RXQ, "unbatched", opts)
+    got = run(tmp_path, RXTXQ, "batched", opts, cpu_max=cpu_max, tag=f"b{cpu_max}")
+    _check(base, got, 30000)
+    r = got["reports"][0]
+    assert r["gpu_calls"] == 1 and r["cpu_calls"] == 0 and r["cpu"] == 0 and r["frames"] == r["queued"] > 5000
+
+
+@pytest.mark.gpu
+def test_rx_tx_small_burst_default_threshold_on_cpu(tmp_path):
+    """A burst of 40 frames (level-ip's usual flush size) with the default
+    threshold: the RX call and the flush both run on the calling thread, and
+    the tap bytes are the unbatched stack's."""
+    opts = {"n": 40, "seed": 7, "kinds": "all"}
+    base = run(tmp_path, RXQ, "unbatched", opts)
+    got = run(tmp_path, RXTXQ, "batched", opts)
+    _check(base, got, 40)
+    r = got["reports"][0]
+    assert r["cpu_calls"] == 1 and r["gpu_calls"] == 0
