@@ -805,6 +805,10 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
                  alloc_skb(BUFLEN) buffer, src/skbuff.c:5-20), the slots in
                  random order over an n x 1616 B buffer (the gather path)
       dma        the slab registered LVLIP_REG_DMA (copy engine reads spans)
+      dma_shuffled  the same registered slab, the frames in shuffled call
+                 order over a slab far larger than the arena (not
+                 dense in order, so gathered frame by frame instead of cut
+                 into one-frame pieces each moving a whole span)
       zerocopy   the slab registered LVLIP_REG_ZEROCOPY (kernel reads in place)
       scattered_t8  scattered with 8 gather threads (LVLIP_GATHER_THREADS;
                  the default is min(hardware threads, 16), round 4's was 8)
@@ -867,14 +871,22 @@ def frames_host(lvlip, dev, host, fd, l4_bytes):
 
     keep_slab = frames_arr(host, fd["offset"].astype(np.uint64))
     keep_scat = frames_arr(scat, slot.astype(np.uint64) * stride)
+    shuf = rng.permutation(n)
+    keep_shuf = frames_arr(host, fd["offset"].astype(np.uint64))
+    keep_shuf[0][:] = keep_shuf[0][shuf]
     d = dev.index or 0
     with lvlip.Context(d, cpu_max=0) as ctx:  # the GPU path (crossover() times both sides)
         run(ctx, keep_slab[1], "slab")
         run(ctx, keep_scat[1], "scattered")
-        for tag, flag in (("dma", lvlip.REG_DMA), ("zerocopy", lvlip.REG_ZEROCOPY)):
+        for tag, flag, arr in (("dma", lvlip.REG_DMA, keep_slab[1]), ("zerocopy", lvlip.REG_ZEROCOPY, keep_slab[1]),
+                               ("dma_shuffled", lvlip.REG_DMA, keep_shuf[1])):
             ctx.register(host, flag)
             try:
-                run(ctx, keep_slab[1], tag)
+                s0 = ctx.stats()
+                run(ctx, arr, tag)
+                s1 = ctx.stats()
+                out[tag]["h2d_bytes_per_call"] = (s1["h2d_bytes"] - s0["h2d_bytes"]) // max(1, s1["gpu_calls"] -
+                                                                                          s0["gpu_calls"])
             finally:
                 ctx.unregister(host)
     for env, tag, arr, flag in (("LVLIP_GATHER_THREADS=8", "scattered_t8", keep_scat[1], None),
@@ -922,7 +934,7 @@ def mixed_frames_host(lvlip, n):
     return host, fd
 
 
-CROSS_N = (1, 3, 8, 64, 512, 4096, 32768, 262144)
+CROSS_N = (1, 3, 8, 64, 512, 2048, 4096, 8192, 16384, 32768, 65536, 262144)
 SKB_DTYPE = np.dtype([("next", "<u8"), ("prev", "<u8"), ("rt", "<u8"), ("dev", "<u8"), ("refcnt", "<i4"),
                       ("protocol", "<u2"), ("pad", "<u2"), ("len", "<u4"), ("dlen", "<u4"), ("seq", "<u4"),
                       ("end_seq", "<u4"), ("end", "<u8"), ("head", "<u8"), ("data", "<u8"),

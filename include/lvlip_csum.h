@@ -274,7 +274,7 @@ int lvlip_csum_unregister(lvlip_csum_ctx *ctx, void *ptr);
  * LVLIP_CPU_MAX when set when the context is created, else
  * LVLIP_CPU_MAX_DEFAULT.  Device-resident calls (Groups 2 and the _dev frame
  * calls) are never dispatched to the CPU. */
-#define LVLIP_CPU_MAX_DEFAULT 2048u
+#define LVLIP_CPU_MAX_DEFAULT 8192u
 int lvlip_csum_ctx_set_cpu_max(lvlip_csum_ctx *ctx, uint32_t cpu_max);
 /* The context's current threshold (0 for a NULL context). */
 uint32_t lvlip_csum_ctx_cpu_max(const lvlip_csum_ctx *ctx);
@@ -285,9 +285,10 @@ typedef struct lvlip_ctx_stats {
     uint64_t gpu_calls;  /* host calls that ran on the GPU                  */
     uint64_t cpu_calls;  /* host calls run on the calling thread (cpu_max)  */
     uint64_t pieces;     /* device pieces launched by the GPU calls         */
-    uint64_t h2d_bytes;  /* packet / frame bytes copied host->device by the
-                            copy engine (descriptors and in-place reads over
-                            PCIe not counted)                              */
+    uint64_t h2d_bytes;  /* bytes the pieces moved host->device: each piece's
+                            gathered arena bytes or copied span, whether the
+                            copy engine or (small pieces, zero-copy) the
+                            kernel moved them; descriptors not counted     */
 } lvlip_ctx_stats;
 int lvlip_csum_ctx_stats(const lvlip_csum_ctx *ctx, lvlip_ctx_stats *out);
 

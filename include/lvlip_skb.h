@@ -60,7 +60,10 @@ typedef struct lvlip_frame {
 
 /* Verdict per frame; frames are not modified.  Must run before ip_init_pkt's
  * in-place byte swaps (src/ip_input.c:47).  n <= LVLIP_MAX_BATCH / 2 (up to two
- * checksums per frame).  Returns 0 or LVLIP_E*. */
+ * checksums per frame).  Returns 0 or LVLIP_E* (LVLIP_ERANGE: with
+ * LVLIP_RX_VERIFY_L4, a frame longer than the context's arena).  A call of at
+ * most the context's cpu_max frames runs on the calling thread
+ * (lvlip_csum_ctx_set_cpu_max, include/lvlip_csum.h), with the same results. */
 int lvlip_rx_verify(lvlip_csum_ctx *ctx, const lvlip_frame *frames, uint32_t n,
                     uint32_t flags, uint8_t *verdict);
 
@@ -88,7 +91,10 @@ void lvlip_rx_apply(uint32_t n, uint8_t *verdict, uint32_t m, const uint32_t *ta
  *   IPv4 : checksum(ih, ihl*4, 0), src/ip_output.c:42,53 (ip_send_check)
  * The IPv4 header checksum does not cover the L4 bytes, so all 2n checksums
  * are one batch; n <= LVLIP_MAX_BATCH / 2.  Returns 0 or LVLIP_E* (frames
- * untouched on error). */
+ * untouched on error): LVLIP_EINVAL for a malformed frame (not IPv4, ihl < 5,
+ * shorter than 14 + its IP length), LVLIP_ERANGE for a frame longer than the
+ * context's arena.  A call of at most the context's cpu_max frames runs on the
+ * calling thread, with the same results and codes. */
 int lvlip_tx_checksum(lvlip_csum_ctx *ctx, lvlip_frame *frames, uint32_t n);
 
 /* Plan: fills iov[]/field[] (capacity 2n; field = where each result goes),
@@ -150,7 +156,8 @@ int lvlip_tx_checksum_skb_list(lvlip_csum_ctx *ctx, struct sk_buff_head *q);
 
 /* The same calls computed by the library's CPU code on the calling thread,
  * with the same results and return codes (LVLIP_EINVAL on a malformed frame,
- * frames untouched; no arena, so never LVLIP_ERANGE).  A context's calls of at
+ * frames untouched; no arena, so LVLIP_ERANGE only for an RX queue longer than
+ * cap).  A context's calls of at
  * most its cpu_max frames run these (lvlip_csum_ctx_set_cpu_max,
  * include/lvlip_csum.h).  A caller that deferred its TX checksums also calls
  * them when the GPU call fails (LVLIP_ENODEV, LVLIP_EHIP, LVLIP_ENOMEM,

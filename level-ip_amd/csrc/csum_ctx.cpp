@@ -59,8 +59,9 @@ int drain(lvlip_csum_ctx* c, Slot& s) {
     return LVLIP_OK;
 }
 
-int count_piece(lvlip_csum_ctx* c) {
+int count_piece(lvlip_csum_ctx* c, uint64_t bytes) {
     c->stats.pieces++;
+    c->stats.h2d_bytes += bytes;
     if (c->fail_piece && ++c->call_pieces == c->fail_piece)
         return fail(c, hipErrorLaunchFailure, "injected failure (LVLIP_FAIL_PIECE)");
     return LVLIP_OK;
@@ -142,7 +143,7 @@ void free_slot(Slot& s) {
 int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uint16_t* user_out,
                  const uint8_t* src = nullptr, const uint8_t* dev_base = nullptr) {
     hipError_t e;
-    if (const int rc = count_piece(c); rc != LVLIP_OK) return rc;
+    if (const int rc = count_piece(c, bytes); rc != LVLIP_OK) return rc;
     lvlip_launch_cfg cfg{};
     cfg.kernel = LVLIP_KERNEL_AUTO;  // the piece's average length picks the kernel
     cfg.len_hint = (int32_t)(bytes / count > 0x7fffffffull ? 0x7fffffff : bytes / count);
@@ -171,7 +172,6 @@ int launch_piece(lvlip_csum_ctx* c, Slot& s, uint64_t bytes, uint32_t count, uin
         const uint64_t nb = src && src != s.h_bytes ? bytes : align16(bytes);
         const int rc = h2d_ordered(c, s, s.d_bytes, src ? src : s.h_bytes, nb, "H2D bytes");
         if (rc != LVLIP_OK) return rc;
-        c->stats.h2d_bytes += nb;
     }
     int rc = lvlip_csum_batch_dev_ex(dev_base ? dev_base : s.d_bytes, s.d_desc, count, s.d_out,
                                      s.stream, &cfg);

@@ -127,9 +127,9 @@ const Region* find_region(const lvlip_csum_ctx* c, const void* p, uint64_t len);
 // records the slot's completion after its piece of `piece_bytes` bytes; the
 // wait for it sleeps from c->block_min bytes up, else spins
 int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes, uint64_t piece_bytes);
-// Counts a device piece of the current call (stats, LVLIP_FAIL_PIECE):
-// LVLIP_OK, or the injected LVLIP_EHIP.
-int count_piece(lvlip_csum_ctx* c);
+// Counts a device piece of the current call moving `bytes` from the host
+// (stats, LVLIP_FAIL_PIECE): LVLIP_OK, or the injected LVLIP_EHIP.
+int count_piece(lvlip_csum_ctx* c, uint64_t bytes);
 // Start of a host call that goes to the GPU (counters, the per-call piece count).
 inline void begin_gpu_call(lvlip_csum_ctx* c) {
     c->stats.gpu_calls++;

@@ -171,7 +171,7 @@ struct FrameSlots {
 int launch_frame_piece(lvlip_csum_ctx* c, Slot& s, int mode, uint64_t bytes, uint32_t k, void* user_out,
                        const uint8_t* src = nullptr, const uint8_t* dev_base = nullptr) {
     hipError_t e;
-    if (const int rc = count_piece(c); rc != LVLIP_OK) return rc;
+    if (const int rc = count_piece(c, bytes); rc != LVLIP_OK) return rc;
     const size_t nout = (size_t)k * out_bytes(mode);
     if (bytes <= c->direct_max && (dev_base || !src)) {
         const int rc = lvlip_frames_host_launch(mode, dev_base ? dev_base : s.dh_bytes,
@@ -191,7 +191,6 @@ int launch_frame_piece(lvlip_csum_ctx* c, Slot& s, int mode, uint64_t bytes, uin
         if ((e = hipMemcpyAsync(s.d_bytes, src ? src : s.h_bytes, nb, hipMemcpyHostToDevice, s.stream)) !=
             hipSuccess)
             return fail(c, e, "H2D frames");
-        c->stats.h2d_bytes += nb;
     }
     const int rc = lvlip_frames_host_launch(mode, dev_base ? dev_base : s.d_bytes,
                                             (const lvlip_frame_desc*)s.d_desc, k, s.d_out, s.stream);

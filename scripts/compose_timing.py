@@ -23,8 +23,8 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = os.path.join(ROOT, "oracle", "_ref")
-BURSTS = [8, 64, 512, 4096, 32768]
-WRITES = [4 << 10, 64 << 10, 1 << 20, 8 << 20]
+BURSTS = [8, 64, 512, 4096, 16384, 32768, 131072]
+WRITES = [4 << 10, 64 << 10, 1 << 20, 8 << 20, 32 << 20]
 
 
 def env_for(cpu_max):

@@ -55,7 +55,8 @@ for step in "$@"; do
     crossover) run crossover 600 python bench.py --crossover --steps 5 --warmup 2 --no-cpu-baseline ;;
     compose) run compose 900 sh -c "python scripts/compose_timing.py > gpurun_out/${TAG}_compose.json" ;;
     dispatch) run dispatch 900 python -u -m pytest tests/test_dispatch_gpu.py tests/test_ref_tx_batch.py \
-                tests/test_ref_rx_batch.py tests/test_ref_scale.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+                tests/test_ref_rx_batch.py tests/test_ref_scale.py tests/test_skb_gpu.py tests/test_skb_list.py \
+                tests/test_sanitize_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     numa) run numa 300 python scripts/lab_numa.py "gpurun_out/${TAG}_numa.json" ;;
     window:*) set_=${step#window:}; run "window_$set_" 400 env LAB_SET="$set_" python scripts/lab_window.py "gpurun_out/${TAG}_window_$set_.json" ;;
     evidence:*|pmc:*)

@@ -72,7 +72,7 @@ class TxqReport(ctypes.Structure):  # oracle/ref_txq.c: struct lvlip_txq_report
 def burst(n, seed, kinds):
     rng = np.random.default_rng(seed)
     ks = list(ref_rx_cases.KINDS) if kinds == "all" else ["ok"]
-    frames = [ARP] + [ref_rx_cases.echo_frame(ks[int(rng.integers(0, len(ks)))], rng, i) for i in range(n)]
+    frames = [ARP] + [ref_rx_cases.echo_frame(ks[int(rng.integers(0, len(ks)))], rng, i % 16384) for i in range(n)]
     off = np.zeros(len(frames), np.uint64)
     ln = np.array([len(f) for f in frames], np.uint32)
     off[1:] = np.cumsum(ln[:-1])

@@ -62,6 +62,8 @@ import struct
 import sys
 import threading
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 for p in (os.path.join(HERE, "golden"), HERE, os.path.join(ROOT, "level-ip_amd"), os.path.join(ROOT, "oracle")):
@@ -211,7 +213,7 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
     addr = struct.pack("=H", socket.AF_INET) + struct.pack("!H", 8000) + bytes(tap_ip) + bytes(8)
     addr_buf = ctypes.create_string_buffer(addr, len(addr))
     lib.tcp_v4_connect(sk, ctypes.addressof(addr_buf), 16, 0)
-    payload = bytes(((7 * i + 3) & 0xFF) for i in range(write_bytes))
+    payload = ((np.arange(write_bytes, dtype=np.uint64) * 7 + 3) & 0xFF).astype(np.uint8).tobytes()
     t0, c0 = time.perf_counter(), time.process_time()
     lib.tcp_send(sk, payload, len(payload))
     lib.tcp_send_next(sk, send_next if send_next > 0 else (write_bytes // 536 + 8))

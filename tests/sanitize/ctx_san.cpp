@@ -74,7 +74,8 @@ static void scattered(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_
 
 // One flat buffer that ends at the last packet's last byte (not a multiple of
 // 16), packets at every alignment with gaps; optionally registered.
-static void flat(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_t seed, int reg, uint32_t gap = 40) {
+static void flat(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_t seed, int reg, uint32_t gap = 40,
+                 bool shuffle = false) {
     Rng r{seed};
     std::vector<lvlip_csum_desc> d(n);
     uint64_t off = 0;
@@ -88,6 +89,10 @@ static void flat(lvlip_csum_ctx* ctx, uint32_t n, uint32_t max_len, uint64_t see
     const size_t bytes = off ? off : 1;
     uint8_t* base = (uint8_t*)malloc(bytes);
     for (size_t b = 0; b < bytes; ++b) base[b] = (uint8_t)r();
+    // out of address order: the span paths would cut one-packet pieces each
+    // moving a whole span, so these go packet by packet (dense_ordered)
+    if (shuffle)
+        for (uint32_t i = n - 1; i > 0; --i) std::swap(d[i], d[r() % (i + 1)]);
     if (reg >= 0)
         CHECK(lvlip_csum_register(ctx, base, bytes, (uint32_t)reg) == LVLIP_OK, "register %d", reg);
     std::vector<uint16_t> out(n, 0);
@@ -244,6 +249,9 @@ int main() {
     // packets spread thinly over a zero-copy region: read in place (a dense
     // batch moves as spans, as from a DMA region)
     flat(ctx, 3000, 1600, 11, (int)LVLIP_REG_ZEROCOPY, 8192);
+    // shuffled descriptors over a slab far larger than the arena: gathered
+    flat(ctx, 20000, 1600, 12, -1, 40, true);
+    flat(ctx, 20000, 1600, 13, (int)LVLIP_REG_DMA, 40, true);
     frame_calls(ctx, 20000, 6);
     frame_slab(ctx, 20000, 7, -1);
     frame_slab(ctx, 20000, 8, (int)LVLIP_REG_DMA);
@@ -251,6 +259,23 @@ int main() {
     // frames spread thinly over a zero-copy region (gaps of up to 8 KiB): read
     // in place rather than moved as spans
     frame_slab(ctx, 3000, 10, (int)LVLIP_REG_ZEROCOPY, 8192);
+
+    // the CPU side of the threshold (lvlip_csum_ctx_set_cpu_max): the same
+    // kinds of batches on the calling thread, over exact-size allocations
+    {
+        lvlip_ctx_stats s0, s1;
+        CHECK(lvlip_csum_ctx_stats(ctx, &s0) == LVLIP_OK, "stats");
+        CHECK(lvlip_csum_ctx_set_cpu_max(ctx, 1u << 30) == LVLIP_OK && lvlip_csum_ctx_cpu_max(ctx) == (1u << 30),
+              "cpu_max");
+        scattered(ctx, 3000, 3000, 21);
+        flat(ctx, 3000, 1600, 22, -1);
+        frame_calls(ctx, 3000, 23);
+        frame_slab(ctx, 3000, 24, -1);
+        CHECK(lvlip_csum_ctx_stats(ctx, &s1) == LVLIP_OK && s1.gpu_calls == s0.gpu_calls &&
+                  s1.cpu_calls > s0.cpu_calls,
+              "cpu side: %llu gpu calls", (unsigned long long)(s1.gpu_calls - s0.gpu_calls));
+        CHECK(lvlip_csum_ctx_set_cpu_max(ctx, 0) == LVLIP_OK, "cpu_max 0");
+    }
 
     // a packet larger than the arena is refused; nothing is read
     std::vector<uint8_t> big((2u << 20) + 5u, 0xab);

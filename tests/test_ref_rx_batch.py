@@ -34,13 +34,19 @@ needs_ref = pytest.mark.skipif(not os.path.exists(ref_rx_cases.REF_SO), reason="
 REF_RXQ = os.path.join(os.path.dirname(ref_rx_cases.REF_SO), "libref_rxq.so")
 
 
-def _run(frames, mode, so=ref_rx_cases.REF_SO):
+def _run(frames, mode, so=ref_rx_cases.REF_SO, cpu_max="0"):
+    """cpu_max: the context's LVLIP_CPU_MAX in the child (None: unset, the
+    library's default threshold, under which these queues of ~100-200 skbs
+    are verified on the calling thread; "0": on the GPU)."""
+    env = {k: v for k, v in os.environ.items() if k != "LVLIP_CPU_MAX"}
+    if cpu_max is not None:
+        env["LVLIP_CPU_MAX"] = cpu_max
     with tempfile.TemporaryDirectory() as d:
         fin, fout = os.path.join(d, "f.json"), os.path.join(d, "o.json")
         with open(fin, "w") as f:
             json.dump([bytes(x).hex() for x in frames], f)
         r = subprocess.run([sys.executable, CHILD, fin, fout, so, mode],
-                           stdin=subprocess.DEVNULL, capture_output=True, text=True, timeout=300)
+                           stdin=subprocess.DEVNULL, capture_output=True, text=True, timeout=300, env=env)
         assert r.returncode == 0, r.stderr[-3000:]
         with open(fout) as f:
             return json.load(f)
@@ -51,9 +57,9 @@ def _frames(seed, per_kind):
     return [ARP] + frs, ["arp"] + kinds
 
 
-def _check(frames, kinds, mode):
+def _check(frames, kinds, mode, cpu_max="0"):
     ref = _run(frames, "unbatched")
-    got = _run(frames, mode)
+    got = _run(frames, mode, cpu_max=cpu_max)
     # the ARP reply, then one echo reply per accepted request
     assert ref["replies"][0] is not None and got["replies"][0] == ref["replies"][0]
     answered = {k for k, r in zip(kinds, ref["replies"]) if r is not None}
@@ -76,14 +82,17 @@ def test_batched_rx_composition_with_oracle_verdicts():
 
 @pytest.mark.gpu
 @needs_ref
-def test_batched_rx_through_reference_stack_on_gpu():
-    """VERDICT r03 Next #3: one lvlip_rx_verify_skb_list on the GPU over the
-    queue, then level-ip's own ip_rcv -> icmpv4_reply -> ip_output for the
-    accepted skbs only.  The replies on the tap are byte-identical to the
-    unbatched reference run on the same frames, and the dropped set equals
-    what ip_rcv itself drops (src/ip_input.c:22-43, :51-60)."""
+@pytest.mark.parametrize("cpu_max", ["0", None])
+def test_batched_rx_through_reference_stack_on_gpu(cpu_max):
+    """VERDICT r03 Next #3: one lvlip_rx_verify_skb_list over the queue (on
+    the GPU with threshold 0; on the calling thread with the library's default
+    threshold, VERDICT r05 Next #1), then level-ip's own ip_rcv ->
+    icmpv4_reply -> ip_output for the accepted skbs only.  The replies on the
+    tap are byte-identical to the unbatched reference run on the same frames,
+    and the dropped set equals what ip_rcv itself drops (src/ip_input.c:22-43,
+    :51-60)."""
     frames, kinds = _frames(82, 24)
-    ref, got = _check(frames, kinds, "batched")
+    ref, got = _check(frames, kinds, "batched", cpu_max)
     assert got["replies"] == ref["replies"]
     dropped = [v not in (lvlip.RX_OK, lvlip.RX_NOT_IP) for v in got["verdicts"]]
     assert dropped == [r is None for r in ref["replies"]]
