@@ -23,7 +23,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = os.path.join(ROOT, "oracle", "_ref")
-BURSTS = [8, 64, 512, 4096, 16384, 32768, 131072]
+BURSTS = [8, 64, 512, 4096, 8192, 16384, 32768, 65536, 131072]
 WRITES = [4 << 10, 64 << 10, 1 << 20, 8 << 20, 32 << 20]
 
 
@@ -34,24 +34,28 @@ def env_for(cpu_max):
     return env
 
 
-def rx(lib, mode, cpu_max=None):
+def rx(lib, mode, cpu_max=None, **extra_env):
+    env = env_for(cpu_max)
+    env.update({k: str(v) for k, v in extra_env.items()})
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "o.json")
         subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ref_scale_child.py"), out,
                         os.path.join(REF, lib), mode, json.dumps({"time": BURSTS, "kinds": "ok", "seed": 3})],
-                       check=True, stdin=subprocess.DEVNULL, env=env_for(cpu_max), timeout=900)
+                       check=True, stdin=subprocess.DEVNULL, env=env, timeout=900)
         with open(out) as f:
             return json.load(f)["time"]
 
 
-def tx(lib, mode, w, cpu_max=None):
+def tx(lib, mode, w, cpu_max=None, **extra_env):
+    env = env_for(cpu_max)
+    env.update({k: str(v) for k, v in extra_env.items()})
     with tempfile.TemporaryDirectory() as d:
         req, out = os.path.join(d, "r.json"), os.path.join(d, "o.json")
         with open(req, "w") as f:
             json.dump([], f)
         subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ref_tx_batch_child.py"), req, out,
                         os.path.join(REF, lib), mode, json.dumps({"write_bytes": w, "send_next": 0, "time": True})],
-                       check=True, stdin=subprocess.DEVNULL, env=env_for(cpu_max), timeout=900)
+                       check=True, stdin=subprocess.DEVNULL, env=env, timeout=900)
         with open(out) as f:
             o = json.load(f)
         r = {"wall_us": round(o["time"]["tcp_wall_s"] * 1e6, 1), "cpu_us": round(o["time"]["tcp_cpu_s"] * 1e6, 1),
@@ -68,11 +72,16 @@ def main():
     for tag, cm in (("batched_default", None), ("batched_gpu", 0), ("batched_cpu", 1 << 30)):
         res["rx"][tag] = rx("libref_rxtxq.so", "batched", cm)
         print("rx", tag, res["rx"][tag], file=sys.stderr, flush=True)
-    for tag, lib, mode, cm in (("unbatched", "libref_fixclock.so", "unbatched", None),
-                               ("batched_default", "libref_txq.so", "gpu", None),
-                               ("batched_gpu", "libref_txq.so", "gpu", 0),
-                               ("batched_cpu", "libref_txq.so", "gpu", 1 << 30)):
-        res["tx"][tag] = {str(w): tx(lib, mode, w, cm) for w in WRITES}
+    # diagnosis: the GPU side with one gather thread (the caller's), so no
+    # frame line moves between cores before the stack touches it again
+    res["rx"]["batched_gpu_t1"] = rx("libref_rxtxq.so", "batched", 0, LVLIP_GATHER_THREADS=1)
+    print("rx batched_gpu_t1", res["rx"]["batched_gpu_t1"], file=sys.stderr, flush=True)
+    for tag, lib, mode, cm, ex in (("unbatched", "libref_fixclock.so", "unbatched", None, {}),
+                                   ("batched_default", "libref_txq.so", "gpu", None, {}),
+                                   ("batched_gpu", "libref_txq.so", "gpu", 0, {}),
+                                   ("batched_cpu", "libref_txq.so", "gpu", 1 << 30, {}),
+                                   ("batched_gpu_t1", "libref_txq.so", "gpu", 0, {"LVLIP_GATHER_THREADS": 1})):
+        res["tx"][tag] = {str(w): tx(lib, mode, w, cm, **ex) for w in WRITES}
         print("tx", tag, res["tx"][tag], file=sys.stderr, flush=True)
     print(json.dumps(res))
 

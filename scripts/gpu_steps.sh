@@ -13,6 +13,7 @@
 #   e2e[:WL]              the bench line with its host-resident (PCIe-inclusive) rates and small-batch latency
 #   frames                the mixed bench line with its device frame-call diag (TX fill, RX verify)
 #   crossover             bench.py --crossover: host calls at n = 1..256K on both sides of the CPU/GPU threshold
+#   crossover_t1          the same with LVLIP_GATHER_THREADS=1 (the gather on the calling thread)
 #   compose               scripts/compose_timing.py: level-ip's own stack per burst / flush, batched and not
 #   dispatch              the round-6 dispatch, failure and composition GPU tests alone
 #   rehearse:N            bench.py --gpus N self-launched over gloo, the ranks sharing the one GPU
@@ -53,6 +54,8 @@ for step in "$@"; do
     rehearse_strong:*) n=${step#rehearse_strong:}; run "rehearse_strong_n$n" 400 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --workload tcp1500x64m --steps 20 --warmup 5 ;;
     rehearse_root:*) n=${step#rehearse_root:}; run "rehearse_root_n$n" 300 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --origin root --steps 50 --warmup 10 ;;
     crossover) run crossover 600 python bench.py --crossover --steps 5 --warmup 2 --no-cpu-baseline ;;
+    crossover_t1) run crossover_t1 600 env LVLIP_GATHER_THREADS=1 python bench.py --crossover --steps 5 --warmup 2 \
+                    --no-cpu-baseline ;;
     compose) run compose 900 sh -c "python scripts/compose_timing.py > gpurun_out/${TAG}_compose.json" ;;
     dispatch) run dispatch 900 python -u -m pytest tests/test_dispatch_gpu.py tests/test_ref_tx_batch.py \
                 tests/test_ref_rx_batch.py tests/test_ref_scale.py tests/test_skb_gpu.py tests/test_skb_list.py \
