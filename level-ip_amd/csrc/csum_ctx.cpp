@@ -459,6 +459,13 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         c->first_piece = v > 0 ? align16((uint64_t)v) : (4ull << 20);
         if (c->first_piece > c->piece) c->first_piece = c->piece;  // the ramp's shifts never overflow
     }
+    // LVLIP_INLINE_MAX: host calls of at most this many packets / frames keep
+    // their host steps on the calling thread (ctx_impl.h; 0: never)
+    {
+        const char* e = getenv("LVLIP_INLINE_MAX");
+        const long long v = e ? atoll(e) : 32768;
+        c->inline_max = v > 0 ? (uint32_t)(v > 0xffffffffll ? 0xffffffffll : v) : 0u;
+    }
     // LVLIP_CPU_MAX: host calls of at most this many packets / frames run on
     // the calling thread (lvlip_csum_ctx_set_cpu_max; 0: always the GPU)
     {
@@ -595,6 +602,7 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
                           uint16_t* out) {
     if (!c || (n && (!pkts || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
+    begin_call(c, n);
     if (first_failure(c, n, [pkts](uint32_t i) { return pkts[i].len > 0 && !pkts[i].ptr ? LVLIP_EINVAL : LVLIP_OK; }) !=
         LVLIP_OK)
         return LVLIP_EINVAL;
@@ -678,6 +686,7 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx* c, const void* base, size_t base_
                                const lvlip_csum_desc* d, uint32_t n, uint16_t* out) {
     if (!c || (n && (!base || !d || !out)) || n > LVLIP_MAX_BATCH) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
+    begin_call(c, n);
     const uint8_t* b = (const uint8_t*)base;
     const uint64_t arena = c->arena;
     const int bad = first_failure(c, n, [d, base_bytes, arena](uint32_t q) {

@@ -103,6 +103,15 @@ struct lvlip_csum_ctx {
     // the error paths (a TX call's undo, a caller's CPU fill) on a healthy GPU
     uint32_t fail_piece = 0;
     uint32_t call_pieces = 0;  // pieces launched by the current call
+    // host calls of at most this many packets / frames do their host steps
+    // (checks, gather, descriptors, TX field stores) on the calling thread
+    // only (LVLIP_INLINE_MAX; 0: never).  Such a call's frames are the
+    // working set the caller has just built and touches again right after
+    // (level-ip's stack): the pool's 16 threads pulled their cache lines to
+    // other cores and made the composed stack up to 2x costlier per frame
+    // ("Where batch-and-dispatch pays")
+    uint32_t inline_max = 32768;
+    bool inline_call = false;  // the current call is one of those
     lvlip_ctx::Slot slot[lvlip_ctx::kSlots];
     std::vector<lvlip_ctx::Region> regions;
     lvlip::GatherPool pool;
@@ -130,6 +139,9 @@ int arm_slot(lvlip_csum_ctx* c, Slot& s, void* user_out, size_t out_bytes, uint6
 // Counts a device piece of the current call moving `bytes` from the host
 // (stats, LVLIP_FAIL_PIECE): LVLIP_OK, or the injected LVLIP_EHIP.
 int count_piece(lvlip_csum_ctx* c, uint64_t bytes);
+// Start of a host call over n packets / frames: whether its host steps stay
+// on the calling thread (inline_max).
+inline void begin_call(lvlip_csum_ctx* c, uint64_t n) { c->inline_call = c->inline_max && n <= c->inline_max; }
 // Start of a host call that goes to the GPU (counters, the per-call piece count).
 inline void begin_gpu_call(lvlip_csum_ctx* c) {
     c->stats.gpu_calls++;
@@ -241,6 +253,10 @@ inline void copy_nt(uint8_t* dst, const uint8_t* src, uint64_t len) {
 // is copied by several of the context's pool threads.
 template <class F>
 void parallel_ranges(lvlip_csum_ctx* c, uint64_t n, uint64_t min_per_thread, F fn) {
+    if (c->inline_call) {  // a cache-sized call: every host step on the calling thread
+        fn(0, n);
+        return;
+    }
     uint64_t t = c->threads > 1 ? (uint64_t)c->threads : 1u;
     if (n / min_per_thread < t) t = n / min_per_thread ? n / min_per_thread : 1u;
     if (t <= 1) {

@@ -573,6 +573,7 @@ int lvlip_rx_verify(lvlip_csum_ctx* ctx, const lvlip_frame* frames, uint32_t n, 
     // two checksums per frame at most: n as the _dev call
     if (!ctx || (n && (!frames || !verdict)) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
+    begin_call(ctx, n);
     const int mode = (flags & LVLIP_RX_VERIFY_L4) ? M_RX_L4 : M_RX;
     // a frame longer than the arena: LVLIP_ERANGE on every path (the header-
     // only call moves at most kHdrWin <= 4096 B of a frame and never refuses)
@@ -589,6 +590,7 @@ int lvlip_rx_verify(lvlip_csum_ctx* ctx, const lvlip_frame* frames, uint32_t n, 
 int lvlip_tx_checksum(lvlip_csum_ctx* ctx, lvlip_frame* frames, uint32_t n) {
     if (!ctx || (n && !frames) || n > LVLIP_MAX_BATCH / 2u) return LVLIP_EINVAL;
     if (n == 0) return LVLIP_OK;
+    begin_call(ctx, n);
     if (n <= ctx->cpu_max) {
         // the calling thread (lvlip_csum_ctx_set_cpu_max), with the GPU
         // path's checks in its order: a NULL or short frame, then a frame

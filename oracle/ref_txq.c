@@ -70,15 +70,17 @@ uint16_t lvlip_txq_deferred_checksum(void *addr, int count, int start_sum)
 }
 
 /* In place of dst_neigh_output (src/ip_output.c:55): queue a copy of the
- * frame.  Returns what tun_write returns for it (netdev_transmit, the frame's
- * length with its Ethernet header), or -1 when out of memory. */
+ * frame, compact: the 14 bytes netdev_transmit will push (src/netdev.c:46)
+ * and skb->data .. skb->end, the IPv4 packet.  Returns what tun_write returns
+ * for it (netdev_transmit, the frame's length with its Ethernet header), or
+ * -1 when out of memory. */
 int lvlip_txq_output(struct sk_buff *skb)
 {
-    const unsigned int size = (unsigned int)(skb->end - skb->head);
+    const unsigned int size = (unsigned int)(skb->end - skb->data) + ETH_LEN;
     struct sk_buff *c = alloc_skb(size);
     if (!c) return -1;
-    memcpy(c->head, skb->head, size);
-    c->data = c->head + (skb->data - skb->head);
+    memcpy(c->head + ETH_LEN, skb->data, size - ETH_LEN);
+    c->data = c->head + ETH_LEN;
     c->len = skb->len;
     c->dlen = skb->dlen;
     c->dev = skb->dev;

@@ -34,13 +34,16 @@ def env_for(cpu_max):
     return env
 
 
-def rx(lib, mode, cpu_max=None, **extra_env):
+def rx(lib, mode, cpu_max=None, slab=0, **extra_env):
     env = env_for(cpu_max)
     env.update({k: str(v) for k, v in extra_env.items()})
+    opts = {"time": BURSTS, "kinds": "ok", "seed": 3}
+    if slab:
+        opts["slab"] = slab
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "o.json")
         subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ref_scale_child.py"), out,
-                        os.path.join(REF, lib), mode, json.dumps({"time": BURSTS, "kinds": "ok", "seed": 3})],
+                        os.path.join(REF, lib), mode, json.dumps(opts)],
                        check=True, stdin=subprocess.DEVNULL, env=env, timeout=900)
         with open(out) as f:
             return json.load(f)["time"]
@@ -72,15 +75,15 @@ def main():
     for tag, cm in (("batched_default", None), ("batched_gpu", 0), ("batched_cpu", 1 << 30)):
         res["rx"][tag] = rx("libref_rxtxq.so", "batched", cm)
         print("rx", tag, res["rx"][tag], file=sys.stderr, flush=True)
-    # diagnosis: the GPU side with one gather thread (the caller's), so no
-    # frame line moves between cores before the stack touches it again
-    res["rx"]["batched_gpu_t1"] = rx("libref_rxtxq.so", "batched", 0, LVLIP_GATHER_THREADS=1)
-    print("rx batched_gpu_t1", res["rx"]["batched_gpu_t1"], file=sys.stderr, flush=True)
+    # the skbs' buffers from one registered slab (oracle/ref_slab.c): the copy
+    # engine moves the bursts, no gather on the CPU
+    for tag, cm in (("slab_default", None), ("slab_gpu", 0), ("slab_cpu", 1 << 30)):
+        res["rx"][tag] = rx("libref_rxtxq_slab.so", "batched", cm, slab=1 << 30)
+        print("rx", tag, res["rx"][tag], file=sys.stderr, flush=True)
     for tag, lib, mode, cm, ex in (("unbatched", "libref_fixclock.so", "unbatched", None, {}),
                                    ("batched_default", "libref_txq.so", "gpu", None, {}),
                                    ("batched_gpu", "libref_txq.so", "gpu", 0, {}),
-                                   ("batched_cpu", "libref_txq.so", "gpu", 1 << 30, {}),
-                                   ("batched_gpu_t1", "libref_txq.so", "gpu", 0, {"LVLIP_GATHER_THREADS": 1})):
+                                   ("batched_cpu", "libref_txq.so", "gpu", 1 << 30, {})):
         res["tx"][tag] = {str(w): tx(lib, mode, w, cm, **ex) for w in WRITES}
         print("tx", tag, res["tx"][tag], file=sys.stderr, flush=True)
     print(json.dumps(res))

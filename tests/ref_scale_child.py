@@ -27,6 +27,12 @@ LIB and MODE:
 The context follows LVLIP_CPU_MAX from the environment (unset: the library's
 default threshold; 0: every call on the GPU).
 
+With oracle/_ref/libref_rxtxq_slab.so and the option "slab": bytes, every
+skb's buffer comes from one slab (oracle/ref_slab.c) that the context
+registers LVLIP_REG_DMA, the allocator INTEGRATION.md §2b'' recommends: the
+batch calls then move the burst's frames with the copy engine instead of
+gathering them on the CPU.
+
 OPTIONS (JSON): {"n": frames in the burst (after one ARP request), "seed",
 "kinds": "all" (every ip_rcv drop reason, tests/ref_rx_cases.py) or "ok" (echo
 requests only), "flags": the RX verify flags, "time": [burst sizes] (tap =
@@ -99,6 +105,10 @@ def main(out_path, so_path, mode, opts_json):
 
         th = threading.Thread(target=reader, daemon=True)
         th.start()
+    if opts.get("slab"):
+        lib.lvlip_slab_init.argtypes = [ctypes.c_size_t]
+        lib.lvlip_slab_base.restype = ctypes.c_void_p
+        assert lib.lvlip_slab_init(int(opts["slab"])) == 0
     lib.netdev_init()
     lib.route_init()
     for fn in ("lvlip_rxq_fill",):
@@ -120,6 +130,9 @@ def main(out_path, so_path, mode, opts_json):
         lib.lvlip_txq_frames.argtypes = [ctypes.POINTER(lvlip.Frame), ctypes.c_int]
         if mode == "batched":
             ctx = lvlip.Context(0)
+            if opts.get("slab"):
+                assert lvlip.lib().lvlip_csum_register(ctx._h, lib.lvlip_slab_base(), int(opts["slab"]),
+                                                       lvlip.REG_DMA) == 0
             if opts.get("time"):  # warm the GPU path (pinned pages, kernel load) before any clock
                 import workloads
 

@@ -18,6 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = os.path.join(ROOT, "oracle", "_ref")
 RXQ = os.path.join(REF, "libref_rxq.so")
 RXTXQ = os.path.join(REF, "libref_rxtxq.so")
+RXTXQ_SLAB = os.path.join(REF, "libref_rxtxq_slab.so")
 CHILD = os.path.join(ROOT, "tests", "ref_scale_child.py")
 
 pytestmark = pytest.mark.skipif(not (os.path.exists(RXQ) and os.path.exists(RXTXQ)),
@@ -78,3 +79,30 @@ def test_rx_tx_small_burst_default_threshold_on_cpu(tmp_path):
     _check(base, got, 40)
     r = got["reports"][0]
     assert r["cpu_calls"] == 1 and r["gpu_calls"] == 0
+
+
+@pytest.mark.skipif(not os.path.exists(RXTXQ_SLAB), reason="oracle/_ref/libref_rxtxq_slab.so not built")
+def test_rx_tx_burst_slab_allocator_oracle(tmp_path):
+    """CPU: the stack with every skb buffer from one slab (oracle/ref_slab.c,
+    alloc_skb / free_skb weakened in a copy of skbuff.o) and the oracle in
+    place of the library: the tap bytes are the unbatched stack's."""
+    opts = {"n": 2000, "seed": 8, "kinds": "all"}
+    base = run(tmp_path, RXQ, "unbatched", opts)
+    _check(base, run(tmp_path, RXTXQ_SLAB, "oracle", dict(opts, slab=1 << 28), tag="slab_oracle"), 2000)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(RXTXQ_SLAB), reason="oracle/_ref/libref_rxtxq_slab.so not built")
+def test_rx_tx_burst_from_registered_slab(tmp_path):
+    """30 000 frames whose skb buffers lie in one slab the context registers
+    (LVLIP_REG_DMA): the RX call and the flush move them with the copy engine
+    (dense and in order: the flush's bytes moved are its frames' span); the
+    tap bytes equal the unbatched stack's."""
+    opts = {"n": 30000, "seed": 9, "kinds": "all"}
+    base = run(tmp_path, RXQ, "unbatched", opts)
+    got = run(tmp_path, RXTXQ_SLAB, "batched", dict(opts, slab=1 << 28), cpu_max=0, tag="slab_gpu")
+    _check(base, got, 30000)
+    r = got["reports"][0]
+    assert r["gpu_calls"] == 1 and r["cpu"] == 0 and r["frames"] == r["queued"] > 5000
+    # the queued replies (~800-B frames in 256-B granules) moved as spans, not gathered
+    assert r["h2d_bytes"] < 3 * 1600 * r["queued"], r
