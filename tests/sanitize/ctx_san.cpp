@@ -240,7 +240,12 @@ int main() {
         return 2;
     }
     lvlip_csum_ctx* ctx = nullptr;
+    // this context's host steps on its pool threads whatever the call's size
+    // (LVLIP_INLINE_MAX 0); the per-thread contexts below keep the default
+    // (calls of up to 32 768 items on the calling thread)
+    setenv("LVLIP_INLINE_MAX", "0", 1);
     CHECK(lvlip_csum_ctx_create(&ctx, 0, 1u << 20) == LVLIP_OK, "ctx_create");
+    unsetenv("LVLIP_INLINE_MAX");
     scattered(ctx, 20000, 3000, 1);   // ~30 MB through a 1 MiB arena: many pieces
     scattered(ctx, 3, 9000, 2);
     flat(ctx, 20000, 1600, 3, -1);

@@ -235,8 +235,11 @@ static void packets(lvlip_csum_ctx* ctx, uint32_t n, uint64_t seed) {
 
 int main() {
     for (int direct = 0; direct < 2; ++direct) {
-        // direct: pieces read in place; else through the H2D / D2H copies
+        // direct: pieces read in place; else through the H2D / D2H copies.
+        // And the host steps on the pool (LVLIP_INLINE_MAX 0) or, for calls
+        // of up to 32 768 items, on the calling thread (the default)
         setenv("LVLIP_DIRECT_MAX", direct ? "4194304" : "0", 1);
+        setenv("LVLIP_INLINE_MAX", direct ? "32768" : "0", 1);
         lvlip_csum_ctx* ctx = nullptr;
         CHECK(lvlip_csum_ctx_create(&ctx, 0, 1u << 20) == LVLIP_OK, "ctx_create");
         scattered(ctx, 12000, 1 + direct);
@@ -248,6 +251,7 @@ int main() {
         CHECK(lvlip_csum_ctx_destroy(ctx) == LVLIP_OK, "destroy");
     }
     unsetenv("LVLIP_DIRECT_MAX");
+    setenv("LVLIP_INLINE_MAX", "0", 1);  // the threads below use their pools
     // one context per thread, at once (the reference's core, IPC and timer
     // threads, src/main.c:83-89)
     std::vector<std::thread> th;
