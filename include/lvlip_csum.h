@@ -274,7 +274,7 @@ int lvlip_csum_unregister(lvlip_csum_ctx *ctx, void *ptr);
  * LVLIP_CPU_MAX when set when the context is created, else
  * LVLIP_CPU_MAX_DEFAULT.  Device-resident calls (Groups 2 and the _dev frame
  * calls) are never dispatched to the CPU. */
-#define LVLIP_CPU_MAX_DEFAULT 8192u
+#define LVLIP_CPU_MAX_DEFAULT 16384u
 int lvlip_csum_ctx_set_cpu_max(lvlip_csum_ctx *ctx, uint32_t cpu_max);
 /* The context's current threshold (0 for a NULL context). */
 uint32_t lvlip_csum_ctx_cpu_max(const lvlip_csum_ctx *ctx);

@@ -91,7 +91,7 @@ class CtxStats(ctypes.Structure):  # include/lvlip_csum.h: lvlip_ctx_stats
 
 # include/lvlip_csum.h: host calls of at most this many packets / frames run on
 # the calling thread unless the context says otherwise (LVLIP_CPU_MAX)
-CPU_MAX_DEFAULT = 8192
+CPU_MAX_DEFAULT = 16384
 
 
 # RX verdicts and flags (include/lvlip_skb.h)
