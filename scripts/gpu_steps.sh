@@ -49,7 +49,7 @@ for step in "$@"; do
     bench:*) wl=${step#bench:}; run "bench_$wl" 300 python bench.py --workload "$wl" ;;
     e2e) run e2e_tcp1500 300 python bench.py --e2e ;;
     e2e:*) wl=${step#e2e:}; run "e2e_$wl" 300 python bench.py --workload "$wl" --e2e ;;
-    frames) run frames 300 python bench.py --workload mixed --frames ;;
+    frames) run frames 600 python bench.py --workload mixed --frames ;;
     rehearse:*) n=${step#rehearse:}; run "rehearse_n$n" 300 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --steps 50 --warmup 10 ;;
     rehearse_strong:*) n=${step#rehearse_strong:}; run "rehearse_strong_n$n" 400 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --workload tcp1500x64m --steps 20 --warmup 5 ;;
     rehearse_root:*) n=${step#rehearse_root:}; run "rehearse_root_n$n" 300 env LVLIP_DIST_BACKEND=gloo python bench.py --gpus "$n" --origin root --steps 50 --warmup 10 ;;

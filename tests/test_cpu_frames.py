@@ -151,3 +151,70 @@ def test_skb_list_cpu_forms():
     assert [ctypes.string_at(s.contents.data, BUFLEN) for s in q2.skbs] == bufs
     for s in q.skbs + q2.skbs:
         ref.free_skb(s)
+
+
+# ------------------------------------------------- property-based (hypothesis) --
+
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+SETTINGS = settings(max_examples=400, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+
+
+@st.composite
+def _frame(draw):
+    """A frame whose header fields hypothesis picks from the values that steer
+    ip_rcv's decisions (ethertype, version, ihl, TTL, protocol, total length
+    against the frame's length), over random bytes, with random checksum
+    fields (valid or not)."""
+    body = bytearray(draw(st.binary(min_size=0, max_size=1600)))
+    f = bytearray(14) + body
+    if len(f) >= 14:
+        f[12:14] = draw(st.sampled_from([b"\x08\x00", b"\x08\x00", b"\x08\x06", b"\x86\xdd"]))
+    if len(f) >= 34:
+        ver = draw(st.sampled_from([4, 4, 4, 6]))
+        ihl = draw(st.integers(0, 15))
+        f[14] = (ver << 4) | ihl
+        f[22] = draw(st.sampled_from([0, 1, 64, 255]))
+        f[23] = draw(st.sampled_from([1, 6, 6, 17]))
+        iplen = draw(st.one_of(st.just(len(f) - 14), st.integers(0, 0xFFFF)))
+        f[16:18] = iplen.to_bytes(2, "big")
+        if draw(st.booleans()):
+            g = bytearray(f)
+            try:
+                skb_oracle.tx_fill(g)  # valid fields where the frame allows them
+                f = g
+            except (IndexError, struct_error):
+                pass
+    return f
+
+
+struct_error = __import__("struct").error
+
+
+@SETTINGS
+@given(frames=st.lists(_frame(), min_size=0, max_size=24), flags=st.sampled_from([0, lvlip.RX_VERIFY_L4]))
+def test_rx_cpu_property(frames, flags):
+    """lvlip_rx_verify_cpu == the oracle's ip_rcv restatement on any frames."""
+    got = lvlip.rx_verify_cpu(frames, flags).tolist()
+    assert got == [skb_oracle.rx_verdict(bytes(f), flags) for f in frames]
+
+
+@SETTINGS
+@given(frames=st.lists(_frame(), min_size=1, max_size=24))
+def test_tx_cpu_property(frames):
+    """lvlip_tx_checksum_cpu: the oracle's fill on every frame when all are
+    well formed (tx_plan's rule), else LVLIP_EINVAL with every frame as it
+    was."""
+    before = [bytes(f) for f in frames]
+    ok = lvlip.tx_plan([bytearray(f) for f in frames]) is not None
+    if ok:
+        lvlip.tx_checksum_cpu(frames)
+        want = [bytearray(b) for b in before]
+        for w in want:
+            skb_oracle.tx_fill(w)
+        assert [bytes(f) for f in frames] == [bytes(w) for w in want]
+    else:
+        with pytest.raises(lvlip.LvlipError) as e:
+            lvlip.tx_checksum_cpu(frames)
+        assert e.value.rc == lvlip.EINVAL and [bytes(f) for f in frames] == before
