@@ -117,6 +117,24 @@ int lvlip_rxq_receive_all(struct sk_buff_head *q)
     return k;
 }
 
+/* The RX batch step as INTEGRATION.md §2b gives it to a maintainer: ONE
+ * lvlip_rx_verify_skb_list over the queue through the context (a queue of at
+ * most the context's cpu_max skbs is verified on this thread by the library,
+ * a longer one on the GPU); when no context could be made, or the GPU call
+ * fails for a device / HIP / memory / arena reason, the same verdicts from the
+ * library's CPU code (lvlip_rx_verify_skb_list_cpu), so a GPU failure never
+ * drops or admits a frame ip_rcv would not.  *cpu is set to 1 for a fallback.
+ * Returns the number of skbs, or LVLIP_E* (a malformed queue, cap too small). */
+int lvlip_rxq_verify(lvlip_csum_ctx *ctx, struct sk_buff_head *q, uint32_t flags, uint8_t *verdict,
+                     uint32_t cap, int *cpu)
+{
+    int rc = ctx ? lvlip_rx_verify_skb_list(ctx, q, flags, verdict, cap) : LVLIP_ENODEV;
+    *cpu = 0;
+    if (rc >= 0 || rc == LVLIP_EINVAL || (ctx && rc == LVLIP_ERANGE && q->qlen > cap)) return rc;
+    *cpu = 1;
+    return lvlip_rx_verify_skb_list_cpu(q, flags, verdict, cap);
+}
+
 /* The batch-and-dispatch loop: verdict[k] belongs to the
  * k-th queued skb (lvlip_rx_verify_skb_list's order); LVLIP_RX_OK -> ip_rcv
  * (gate: its header marked first, so :38 takes the batch's result),

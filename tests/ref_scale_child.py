@@ -124,6 +124,8 @@ def main(out_path, so_path, mode, opts_json):
         import lvlip
 
         lib.lvlip_rxq_dispatch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        lib.lvlip_rxq_verify.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.POINTER(ctypes.c_int)]
         lib.lvlip_txq_fill.argtypes = [ctypes.c_void_p, ctypes.POINTER(TxqReport)]
         lib.lvlip_txq_send.restype = ctypes.c_int
         lib.lvlip_txq_len.restype = ctypes.c_int
@@ -155,8 +157,9 @@ def main(out_path, so_path, mode, opts_json):
             assert lib.lvlip_rxq_receive_all(ctypes.addressof(q)) == n
             return time.perf_counter() - t0, time.process_time() - c0, None
         v = np.zeros(n, np.uint8)
+        rx_cpu = ctypes.c_int(0)
         if mode == "batched":
-            m = lvlip.lib().lvlip_rx_verify_skb_list(ctx._h, ctypes.addressof(q), flags, v.ctypes.data, n)
+            m = lib.lvlip_rxq_verify(ctx._h, ctypes.addressof(q), flags, v.ctypes.data, n, ctypes.byref(rx_cpu))
             assert m == n, m
         else:
             import skb_oracle
@@ -182,7 +185,8 @@ def main(out_path, so_path, mode, opts_json):
             rep.frames = nq
         assert lib.lvlip_txq_send() == rep.frames
         wall, cpu = time.perf_counter() - t0, time.process_time() - c0
-        r = {"queued": nq, "frames": rep.frames, "rc": rep.rc, "cpu": rep.cpu, "dropped": rep.dropped}
+        r = {"queued": nq, "frames": rep.frames, "rc": rep.rc, "cpu": rep.cpu, "dropped": rep.dropped,
+             "rx_cpu_fallback": rx_cpu.value}
         if s0 is not None:
             s1 = ctx.stats()
             r.update({k: s1[k] - s0[k] for k in ("gpu_calls", "cpu_calls", "pieces", "h2d_bytes")})

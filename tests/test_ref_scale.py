@@ -25,10 +25,11 @@ pytestmark = pytest.mark.skipif(not (os.path.exists(RXQ) and os.path.exists(RXTX
                                 reason="oracle/_ref/libref_{rxq,rxtxq}.so not built")
 
 
-def run(tmp_path, lib, mode, opts, cpu_max=None, tag=None):
-    env = {k: v for k, v in os.environ.items() if k != "LVLIP_CPU_MAX"}
+def run(tmp_path, lib, mode, opts, cpu_max=None, tag=None, **extra_env):
+    env = {k: v for k, v in os.environ.items() if k not in ("LVLIP_CPU_MAX", "LVLIP_FAIL_PIECE")}
     if cpu_max is not None:
         env["LVLIP_CPU_MAX"] = str(cpu_max)
+    env.update({k: str(v) for k, v in extra_env.items()})
     out = tmp_path / f"{tag or mode}.json"
     r = subprocess.run([sys.executable, CHILD, str(out), lib, mode, json.dumps(opts)], stdin=subprocess.DEVNULL,
                        capture_output=True, text=True, timeout=600, env=env)
@@ -111,3 +112,18 @@ def test_rx_tx_burst_from_registered_slab(tmp_path):
     assert r["gpu_calls"] == 1 and r["cpu"] == 0 and r["frames"] == r["queued"] > 5000
     # the queued replies (~800-B frames in 256-B granules) moved as spans, not gathered
     assert r["h2d_bytes"] < 3 * 1600 * r["queued"], r
+
+
+@pytest.mark.gpu
+def test_rx_tx_burst_gpu_failure_falls_back(tmp_path):
+    """Every GPU call of the burst fails (LVLIP_FAIL_PIECE=1): the RX verify
+    (lvlip_rxq_verify, oracle/ref_rxq.c) and the TX flush (lvlip_txq_fill)
+    both fall back to the library's CPU code, and the tap bytes are still the
+    unbatched stack's: a GPU failure neither drops, admits nor sends a frame
+    differently (failure detection)."""
+    opts = {"n": 3000, "seed": 10, "kinds": "all"}
+    base = run(tmp_path, RXQ, "unbatched", opts)
+    got = run(tmp_path, RXTXQ, "batched", opts, cpu_max=0, tag="fail", LVLIP_FAIL_PIECE=1)
+    _check(base, got, 3000)
+    r = got["reports"][0]
+    assert r["rx_cpu_fallback"] == 1 and r["cpu"] == 1 and r["rc"] == -3 and r["frames"] == r["queued"], r
