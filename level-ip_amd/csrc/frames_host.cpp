@@ -551,7 +551,7 @@ struct TxApply final : PieceDone {
 
 // Whether a frame is longer than the context's arena (the frame calls'
 // LVLIP_ERANGE, on every path and on both sides of cpu_max).
-bool first_too_long(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n) {
+bool any_too_long(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n) {
     std::atomic<bool> big{false};
     const uint64_t arena = c->arena;
     parallel_ranges(c, n, 65536, [&big, fr, arena](uint64_t lo, uint64_t hi) {
@@ -577,7 +577,7 @@ int lvlip_rx_verify(lvlip_csum_ctx* ctx, const lvlip_frame* frames, uint32_t n, 
     const int mode = (flags & LVLIP_RX_VERIFY_L4) ? M_RX_L4 : M_RX;
     // a frame longer than the arena: LVLIP_ERANGE on every path (the header-
     // only call moves at most kHdrWin <= 4096 B of a frame and never refuses)
-    if (mode == M_RX_L4 && first_too_long(ctx, frames, n)) return LVLIP_ERANGE;
+    if (mode == M_RX_L4 && any_too_long(ctx, frames, n)) return LVLIP_ERANGE;
     if (n <= ctx->cpu_max) {  // the calling thread (lvlip_csum_ctx_set_cpu_max)
         ctx->stats.cpu_calls++;
         return lvlip_rx_verify_cpu(frames, n, flags, verdict);
@@ -597,7 +597,7 @@ int lvlip_tx_checksum(lvlip_csum_ctx* ctx, lvlip_frame* frames, uint32_t n) {
         // longer than the arena, then a malformed one (the CPU call)
         for (uint32_t i = 0; i < n; ++i)
             if (!frames[i].head || frames[i].len < kEth + 20u) return LVLIP_EINVAL;
-        if (first_too_long(ctx, frames, n)) return LVLIP_ERANGE;
+        if (any_too_long(ctx, frames, n)) return LVLIP_ERANGE;
         ctx->stats.cpu_calls++;
         return lvlip_tx_checksum_cpu(frames, n);
     }
@@ -618,7 +618,7 @@ int lvlip_tx_checksum(lvlip_csum_ctx* ctx, lvlip_frame* frames, uint32_t n) {
         if (b) bad.store(true, std::memory_order_relaxed);
     });
     if (bad.load(std::memory_order_relaxed)) return LVLIP_EINVAL;
-    if (first_too_long(ctx, frames, n)) return LVLIP_ERANGE;
+    if (any_too_long(ctx, frames, n)) return LVLIP_ERANGE;
     TxApply ap(ctx, frames, rec, undo);
     int rc = frames_run(ctx, frames, n, M_TX, (uint8_t*)rec, &ap);
     if (rc == LVLIP_OK && ap.bad) rc = LVLIP_EINVAL;
