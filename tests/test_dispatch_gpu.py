@@ -230,3 +230,34 @@ def test_dma_region_spans_only_in_order(shuffled):
             assert moved <= 1.3 * frame_bytes + (1 << 20), (moved, frame_bytes)
         finally:
             ctx.unregister(buf)
+
+
+@pytest.mark.parametrize("inline_max", ["0", "32768"])
+def test_inline_and_pool_host_steps_agree(inline_max, monkeypatch):
+    """LVLIP_INLINE_MAX: the same 20 000 frames and 40 000 packets with every
+    host step on the pool threads (0) and on the calling thread (the default,
+    calls of up to 32 768 items): the same fills, verdicts and checksums, equal
+    to the oracle, from plain memory and from a registered slab."""
+    monkeypatch.setenv("LVLIP_INLINE_MAX", inline_max)
+    fr = workloads.frames(20000, seed=150, max_l4=1460)
+    want = [bytearray(f) for f in fr]
+    for f in want:
+        skb_oracle.tx_fill(f)
+    buf, fd, views, perm = _slab(fr)
+    with lvlip.Context(0, arena_bytes=4 << 20, cpu_max=0) as ctx:
+        scattered = [bytearray(f) for f in fr]
+        ctx.tx_checksum(scattered)
+        assert [bytes(f) for f in scattered] == [bytes(w) for w in want]
+        ctx.register(buf, lvlip.REG_DMA)
+        try:
+            ctx.tx_checksum(views)
+            assert [bytes(v) for v in views] == [bytes(w) for w in want]
+            for flags in (0, lvlip.RX_VERIFY_L4):
+                v = ctx.rx_verify(views, flags)
+                assert v.tolist() == [skb_oracle.rx_verdict(bytes(w), flags) for w in want], flags
+        finally:
+            ctx.unregister(buf)
+        seg = [bytes(w[14:]) for w in want] * 2
+        got = ctx.batch_host(seg, [0] * len(seg))
+        ref = np.array([pyoracle.checksum(s or b"\0", len(s), 0) for s in seg], np.uint16)
+        assert np.array_equal(got, ref)
