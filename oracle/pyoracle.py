@@ -99,12 +99,16 @@ def _i32(x: int) -> int:
 def checksum(buf, count: Optional[int] = None, start_sum: int = 0) -> int:
     a = _u8(buf)
     count = a.size if count is None else count
+    if count > a.size:  # the C oracle would read past the buffer (count <= 0 reads nothing)
+        raise ValueError(f"count {count} outside a {a.size}-byte buffer")
     return int(liblib().oracle_checksum(a.ctypes.data if a.size else None, count, _i32(start_sum)))
 
 
 def sum_every_16bits(buf, count: Optional[int] = None) -> int:
     a = _u8(buf)
     count = a.size if count is None else count
+    if count > a.size:
+        raise ValueError(f"count {count} outside a {a.size}-byte buffer")
     return int(liblib().oracle_sum_every_16bits(a.ctypes.data if a.size else None, count))
 
 

@@ -101,6 +101,7 @@ static struct sk_buff *pop(struct sk_buff_head *q)
 {
     struct sk_buff *skb = list_first_entry(&q->head, struct sk_buff, list);
     list_del(&skb->list);
+    list_init(&skb->list); /* on no list now (ref_txq.c's hold mode frees such an skb after sending its reply) */
     q->qlen--;
     return skb;
 }

@@ -8,7 +8,9 @@
                 default threshold and with threshold 0 (always the GPU)
   TX            tests/ref_tx_batch_child.py in time mode: one tcp_send of
                 W bytes (smss 536) sent by tcp_send_next, then the flush,
-                for W = 4 KiB .. 8 MiB, unbatched and batched (both thresholds)
+                for W = 4 KiB .. 32 MiB, unbatched and batched (both thresholds)
+  hold_*        the same batched stacks with the TX queue holding each skb by
+                reference instead of copying it (oracle/ref_txq.c's hold mode)
 
 The tap is /dev/null; each figure is the best of 3 after an untimed run of
 the same size (RX), or one run per process (TX).  Prints one JSON object.
@@ -34,12 +36,14 @@ def env_for(cpu_max):
     return env
 
 
-def rx(lib, mode, cpu_max=None, slab=0, **extra_env):
+def rx(lib, mode, cpu_max=None, slab=0, hold=False, **extra_env):
     env = env_for(cpu_max)
     env.update({k: str(v) for k, v in extra_env.items()})
     opts = {"time": BURSTS, "kinds": "ok", "seed": 3}
     if slab:
         opts["slab"] = slab
+    if hold:
+        opts["hold"] = 1
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "o.json")
         subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ref_scale_child.py"), out,
@@ -49,7 +53,7 @@ def rx(lib, mode, cpu_max=None, slab=0, **extra_env):
             return json.load(f)["time"]
 
 
-def tx(lib, mode, w, cpu_max=None, **extra_env):
+def tx(lib, mode, w, cpu_max=None, hold=False, **extra_env):
     env = env_for(cpu_max)
     env.update({k: str(v) for k, v in extra_env.items()})
     with tempfile.TemporaryDirectory() as d:
@@ -57,7 +61,7 @@ def tx(lib, mode, w, cpu_max=None, **extra_env):
         with open(req, "w") as f:
             json.dump([], f)
         subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ref_tx_batch_child.py"), req, out,
-                        os.path.join(REF, lib), mode, json.dumps({"write_bytes": w, "send_next": 0, "time": True})],
+                        os.path.join(REF, lib), mode, json.dumps({"write_bytes": w, "send_next": 0, "time": True, "hold": hold})],
                        check=True, stdin=subprocess.DEVNULL, env=env, timeout=900)
         with open(out) as f:
             o = json.load(f)
@@ -80,10 +84,21 @@ def main():
     for tag, cm in (("slab_default", None), ("slab_gpu", 0), ("slab_cpu", 1 << 30)):
         res["rx"][tag] = rx("libref_rxtxq_slab.so", "batched", cm, slab=1 << 30)
         print("rx", tag, res["rx"][tag], file=sys.stderr, flush=True)
+    # the replies held by reference, not copied into the TX queue
+    for tag, lib, cm, slab in (("hold_default", "libref_rxtxq.so", None, 0), ("hold_gpu", "libref_rxtxq.so", 0, 0),
+                               ("hold_cpu", "libref_rxtxq.so", 1 << 30, 0),
+                               ("slab_hold_default", "libref_rxtxq_slab.so", None, 1 << 30),
+                               ("slab_hold_gpu", "libref_rxtxq_slab.so", 0, 1 << 30),
+                               ("slab_hold_cpu", "libref_rxtxq_slab.so", 1 << 30, 1 << 30)):
+        res["rx"][tag] = rx(lib, "batched", cm, slab=slab, hold=True)
+        print("rx", tag, res["rx"][tag], file=sys.stderr, flush=True)
     for tag, lib, mode, cm, ex in (("unbatched", "libref_fixclock.so", "unbatched", None, {}),
                                    ("batched_default", "libref_txq.so", "gpu", None, {}),
                                    ("batched_gpu", "libref_txq.so", "gpu", 0, {}),
-                                   ("batched_cpu", "libref_txq.so", "gpu", 1 << 30, {})):
+                                   ("batched_cpu", "libref_txq.so", "gpu", 1 << 30, {}),
+                                   ("hold_default", "libref_txq.so", "gpu", None, {"hold": True}),
+                                   ("hold_gpu", "libref_txq.so", "gpu", 0, {"hold": True}),
+                                   ("hold_cpu", "libref_txq.so", "gpu", 1 << 30, {"hold": True})):
         res["tx"][tag] = {str(w): tx(lib, mode, w, cm, **ex) for w in WRITES}
         print("tx", tag, res["tx"][tag], file=sys.stderr, flush=True)
     print(json.dumps(res))

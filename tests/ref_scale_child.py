@@ -33,6 +33,11 @@ registers LVLIP_REG_DMA, the allocator INTEGRATION.md §2b'' recommends: the
 batch calls then move the burst's frames with the copy engine instead of
 gathering them on the CPU.
 
+With the option "hold", the TX queue holds each reply's skb (the RX skb
+icmpv4_reply answered in) by reference instead of copying it
+(lvlip_txq_set_hold, oracle/ref_txq.c): the flush fills the held frames with
+ONE lvlip_tx_checksum, sends them and frees the skbs.
+
 OPTIONS (JSON): {"n": frames in the burst (after one ARP request), "seed",
 "kinds": "all" (every ip_rcv drop reason, tests/ref_rx_cases.py) or "ok" (echo
 requests only), "flags": the RX verify flags, "time": [burst sizes] (tap =
@@ -130,8 +135,12 @@ def main(out_path, so_path, mode, opts_json):
         lib.lvlip_txq_send.restype = ctypes.c_int
         lib.lvlip_txq_len.restype = ctypes.c_int
         lib.lvlip_txq_frames.argtypes = [ctypes.POINTER(lvlip.Frame), ctypes.c_int]
+        lib.lvlip_txq_set_ctx.argtypes = [ctypes.c_void_p]
+        if opts.get("hold"):
+            assert lib.lvlip_txq_set_hold(1) == 0
         if mode == "batched":
             ctx = lvlip.Context(0)
+            lib.lvlip_txq_set_ctx(ctx._h)
             if opts.get("slab"):
                 assert lvlip.lib().lvlip_csum_register(ctx._h, lib.lvlip_slab_base(), int(opts["slab"]),
                                                        lvlip.REG_DMA) == 0

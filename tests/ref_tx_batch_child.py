@@ -36,6 +36,10 @@ OPTIONS (JSON, all optional):
   device       the context's device (default 0; an invalid index makes
                lvlip_csum_ctx_create fail, so the flush fills on the CPU)
   hashes       report frames as sha1 hex digests instead of their bytes
+  hold         the queue holds each skb by reference instead of copying it
+               (lvlip_txq_set_hold, oracle/ref_txq.c): the flush fills the
+               frame array with ONE lvlip_tx_checksum, and a retransmit
+               (skb_reset_header) flushes a held frame before rewriting it
   time         the tap is /dev/null and OUT.json gets the wall and CPU time
                of the TCP phase (sends + flush) and the echo phase; the
                context is made (and its GPU path warmed) before the clock
@@ -52,7 +56,9 @@ end of a socketpair; a reader thread collects every frame the stack writes, in
 order.  OUT.json: {"frames": frames in tap order (hex, or sha1 with hashes),
 "batches": frames per flush, "deferred": CPU checksum computations the TX path
 deferred per flush, "reports": per flush the fill's report and the context's
-counters, "untouched": the malformed queue's check, "time": the timings}.
+counters, "untouched": the malformed queue's check, "early_frames" / "reheld": the
+frames the hold mode sent before a retransmit rewrote them, and those it lost
+(0), "time": the timings}.
 """
 import ctypes
 import json
@@ -129,6 +135,11 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
         lib.lvlip_txq_deferred.restype = ctypes.c_ulong
         lib.lvlip_txq_queue.restype = ctypes.c_void_p
         lib.lvlip_txq_inject.argtypes = [ctypes.c_char_p, ctypes.c_uint]
+        lib.lvlip_txq_set_ctx.argtypes = [ctypes.c_void_p]
+        lib.lvlip_txq_early_frames.restype = ctypes.c_ulong
+        lib.lvlip_txq_reheld.restype = ctypes.c_ulong
+        if opts.get("hold"):
+            assert lib.lvlip_txq_set_hold(1) == 0
     ctxs = []
 
     def context():
@@ -139,6 +150,7 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
         if not ctxs:
             try:
                 ctxs.append(lvlip.Context(int(opts.get("device", 0))))
+                lib.lvlip_txq_set_ctx(ctxs[0]._h)
             except lvlip.LvlipError as e:
                 out["context_error"] = e.rc
                 ctxs.append(None)
@@ -159,7 +171,12 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
             if opts.get("inject") and "untouched" not in out and ctx is not None:
                 # the batch call itself on the queue with its malformed frame
                 before = queued_bytes()
-                rc = lvlip.lib().lvlip_tx_checksum_skb_list(ctx._h, lib.lvlip_txq_queue())
+                if opts.get("hold"):
+                    arr = (lvlip.Frame * n)()
+                    assert lib.lvlip_txq_frames(arr, n) == n
+                    rc = lvlip.lib().lvlip_tx_checksum(ctx._h, arr, n)
+                else:
+                    rc = lvlip.lib().lvlip_tx_checksum_skb_list(ctx._h, lib.lvlip_txq_queue())
                 out["untouched"] = {"rc": rc, "same": queued_bytes() == before}
             s0 = ctx.stats() if ctx is not None else None
             rep = TxqReport()
@@ -245,6 +262,8 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
         if c is not None:
             c.close()
     out.update({"frames": got, "batches": batches, "deferred": deferred, "reports": reports})
+    if batched:
+        out.update({"early_frames": int(lib.lvlip_txq_early_frames()), "reheld": int(lib.lvlip_txq_reheld())})
     if timing:
         out["time"] = {"tcp_wall_s": t_tcp[0], "tcp_cpu_s": t_tcp[1], "echo_wall_s": t_echo[0],
                        "echo_cpu_s": t_echo[1]}

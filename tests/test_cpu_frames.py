@@ -179,12 +179,13 @@ def _frame(draw):
         f[23] = draw(st.sampled_from([1, 6, 6, 17]))
         iplen = draw(st.one_of(st.just(len(f) - 14), st.integers(0, 0xFFFF)))
         f[16:18] = iplen.to_bytes(2, "big")
-        if draw(st.booleans()):
+        # valid fields where the frame holds the packet its header describes
+        if draw(st.booleans()) and 20 <= ihl * 4 <= iplen <= len(f) - 14:
             g = bytearray(f)
             try:
-                skb_oracle.tx_fill(g)  # valid fields where the frame allows them
+                skb_oracle.tx_fill(g)
                 f = g
-            except (IndexError, struct_error):
+            except (IndexError, ValueError, struct_error):
                 pass
     return f
 

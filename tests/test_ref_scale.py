@@ -127,3 +127,30 @@ def test_rx_tx_burst_gpu_failure_falls_back(tmp_path):
     _check(base, got, 3000)
     r = got["reports"][0]
     assert r["rx_cpu_fallback"] == 1 and r["cpu"] == 1 and r["rc"] == -3 and r["frames"] == r["queued"], r
+
+
+def test_rx_tx_burst_hold_oracle(tmp_path):
+    """CPU: the replies held by reference (no copy; oracle/ref_txq.c's hold
+    mode) and filled by the oracle: the tap bytes are the unbatched stack's,
+    and every reply's skb is freed by the flush (the run ends cleanly)."""
+    opts = {"n": 2000, "seed": 11, "kinds": "all"}
+    base = run(tmp_path, RXQ, "unbatched", opts)
+    _check(base, run(tmp_path, RXTXQ, "oracle", dict(opts, hold=1), tag="hold_oracle"), 2000)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cpu_max", [None, 0])
+def test_rx_tx_burst_hold_at_scale(tmp_path, cpu_max):
+    """30 000 frames, the replies held by reference: one RX call, the
+    dispatch, one lvlip_tx_checksum over the held replies; tap bytes equal
+    the unbatched stack's with either threshold."""
+    import lvlip
+
+    opts = {"n": 30000, "seed": 12, "kinds": "all", "hold": 1}
+    base = run(tmp_path, RXQ, "unbatched", opts)
+    got = run(tmp_path, RXTXQ, "batched", opts, cpu_max=cpu_max, tag=f"hold{cpu_max}")
+    _check(base, got, 30000)
+    r = got["reports"][0]
+    assert r["cpu"] == 0 and r["frames"] == r["queued"] > 5000
+    on_gpu = cpu_max == 0 or r["queued"] > lvlip.CPU_MAX_DEFAULT
+    assert (r["gpu_calls"], r["cpu_calls"]) == ((1, 0) if on_gpu else (0, 1)), r

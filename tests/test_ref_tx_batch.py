@@ -47,7 +47,9 @@ def _run(tmp_path, lib, mode, opts=None, env=None, tag=None):
     subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ref_tx_batch_child.py"), str(req), str(out),
                     lib, mode, json.dumps(opts or {})], check=True, stdin=subprocess.DEVNULL, timeout=300,
                    env=env)
-    return json.loads(out.read_text())
+    got = json.loads(out.read_text())
+    got["hold"] = bool((opts or {}).get("hold"))
+    return got
 
 
 def _env(cpu_max=None, **extra):
@@ -66,10 +68,14 @@ def _check_same(base, got, first_batch=8):
     assert not bad, bad[:5]
     # ARP reply, the TCP frames, then one reply per answered request
     assert len(base["frames"]) > 1 + 8 + 4
-    assert got["batches"][0] == first_batch
+    # holding: the SYN went out early, when tcp_send_next's skb_reset_header
+    # was about to rewrite it (the flush before a retransmit)
+    early = got["early_frames"]
+    assert got["reheld"] == 0 and early == (1 if got.get("hold") else 0)
+    assert got["batches"][0] == first_batch - early
     # every batched frame deferred two CPU checksum computations (TCP or ICMP,
     # and the IPv4 header)
-    assert got["deferred"] == [2 * k for k in got["batches"]] or any(r["dropped"] for r in got["reports"])
+    assert sum(got["deferred"]) == 2 * (sum(got["batches"]) + early) or any(r["dropped"] for r in got["reports"])
 
 
 def test_tx_batch_oracle_fill_matches_unbatched_stack(tmp_path):
@@ -165,3 +171,63 @@ def test_tx_batch_at_scale(tmp_path):
     assert got["untouched"] == {"rc": -1, "same": True}
     assert got["frames"] == base["frames"]
     assert got["reports"][0]["dropped"] == 1
+
+
+# --- holding the skbs by reference instead of copying them (oracle/ref_txq.c) ---
+
+HOLD = {"hold": True}
+
+
+def test_tx_batch_hold_oracle_fill_matches_unbatched_stack(tmp_path):
+    """CPU: the queue holds each skb itself (its refcnt raised, so the
+    caller's free_skb is a no-op; no copy), the oracle fills the held frames,
+    the flush sends and releases them, and the SYN the stack retransmits is
+    sent before skb_reset_header rewrites it.  The tap bytes equal the
+    unbatched stack's."""
+    base = _run(tmp_path, FIXCLOCK, "unbatched")
+    _check_same(base, _run(tmp_path, TXQ, "oracle", HOLD, tag="hold_oracle"))
+
+
+def test_tx_batch_hold_no_context_fills_on_cpu(tmp_path):
+    """CPU: held frames, no context: every flush (the early one before the SYN
+    retransmit included) fills on the CPU, same tap bytes."""
+    base = _run(tmp_path, FIXCLOCK, "unbatched")
+    got = _run(tmp_path, TXQ, "gpu", dict(HOLD, device=99), env=_env(0), tag="hold_nodev")
+    _check_same(base, got)
+    assert [(r["rc"], r["cpu"], r["dropped"]) for r in got["reports"]] == [(-2, 1, 0)] * 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cpu_max", [None, 0])
+def test_tx_batch_hold_gpu_fill_matches_unbatched_stack(tmp_path, cpu_max):
+    """Held frames filled by ONE lvlip_tx_checksum per flush (the frame-array
+    call over {data - 14, len + 14}): on the calling thread with the default
+    threshold, on the GPU with 0; tap bytes identical.  With a malformed frame
+    injected the call refuses the array untouched and the flush drops it."""
+    base = _run(tmp_path, FIXCLOCK, "unbatched")
+    got = _run(tmp_path, TXQ, "gpu", HOLD, env=_env(cpu_max), tag=f"hold{cpu_max}")
+    _check_same(base, got)
+    want = (0, 1) if cpu_max == 0 else (1, 0)
+    assert [(r["cpu_calls"], r["gpu_calls"]) for r in got["reports"]] == [want] * 2
+    assert not any(r["cpu"] or r["dropped"] for r in got["reports"])
+    got = _run(tmp_path, TXQ, "gpu", dict(HOLD, inject=True), env=_env(cpu_max), tag=f"hold_inject{cpu_max}")
+    assert got["untouched"] == {"rc": -1, "same": True}
+    _check_same(base, got)
+    assert got["reports"][0]["dropped"] == 1 and got["reports"][1]["dropped"] == 0
+
+
+@pytest.mark.gpu
+def test_tx_batch_hold_at_scale(tmp_path):
+    """The 12 MiB tcp_send with the skbs held: the flush's 23 000+ frames are
+    the write queue's own skbs (no copy), filled by one multi-piece GPU call
+    (threshold 0 and the default) or, when the call fails (LVLIP_FAIL_PIECE),
+    on the CPU; tap bytes identical, and the write queue keeps its skbs
+    (nothing freed twice: the run ends cleanly)."""
+    base = _run(tmp_path, FIXCLOCK, "unbatched", SCALE)
+    n_tcp = 1 + 2 + (SCALE["write_bytes"] + 535) // 536 + 2
+    for cpu_max, extra in ((None, {}), (0, {}), (0, {"LVLIP_FAIL_PIECE": 1})):
+        got = _run(tmp_path, TXQ, "gpu", dict(SCALE, hold=True), env=_env(cpu_max, **extra),
+                   tag=f"hold_scale{cpu_max}{len(extra)}")
+        _check_same(base, got, first_batch=n_tcp - 1)
+        r = got["reports"][0]
+        assert r["gpu_calls"] == 1 and r["pieces"] >= 2 and r["cpu"] == (1 if extra else 0), r
