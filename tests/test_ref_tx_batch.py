@@ -230,4 +230,5 @@ def test_tx_batch_hold_at_scale(tmp_path):
                    tag=f"hold_scale{cpu_max}{len(extra)}")
         _check_same(base, got, first_batch=n_tcp - 1)
         r = got["reports"][0]
-        assert r["gpu_calls"] == 1 and r["pieces"] >= 2 and r["cpu"] == (1 if extra else 0), r
+        # the injected failure stops the call at its first piece
+        assert r["gpu_calls"] == 1 and r["pieces"] >= (1 if extra else 2) and r["cpu"] == (1 if extra else 0), r
