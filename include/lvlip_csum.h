@@ -204,7 +204,10 @@ typedef struct lvlip_csum_ctx lvlip_csum_ctx;
 /* Creates a context on HIP device `device` with a pinned host arena and a
  * device arena of `arena_bytes` each (0 = 64 MiB), and its own stream.
  * A context is owned by one thread at a time (src/main.c:83-89 runs the
- * checksum from several threads: give each its own context). */
+ * checksum from several threads: give each its own context).  Creation also
+ * starts the copy engine (1 MiB each way per slot, LVLIP_WARM_BYTES), so the
+ * first call that copies does not pay its start-up (~7 ms).  Returns 0,
+ * LVLIP_ENODEV, LVLIP_ENOMEM (an arena allocation failed) or LVLIP_EHIP. */
 int lvlip_csum_ctx_create(lvlip_csum_ctx **out, int device,
                           size_t arena_bytes);
 int lvlip_csum_ctx_destroy(lvlip_csum_ctx *ctx);

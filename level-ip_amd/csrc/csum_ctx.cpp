@@ -522,6 +522,30 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
             return LVLIP_ENOMEM;
         }
     }
+    // Start the copy engine now: the first piece that goes through it (a call
+    // larger than direct_max) otherwise pays its start-up, ~7 ms measured on
+    // the first 15K-frame TX call of a context against 0.9 ms for the next.
+    // Each slot copies `warm` bytes of its arena each way once
+    // (LVLIP_WARM_BYTES, default 1 MiB; 0 skips it).
+    {
+        size_t warm = 1u << 20;
+        if (const char* e = getenv("LVLIP_WARM_BYTES")) warm = strtoull(e, nullptr, 10);
+        if (warm > arena_bytes) warm = arena_bytes;
+        hipError_t e = hipSuccess;
+        for (auto& s : c->slot) {
+            if (!warm || e != hipSuccess) break;
+            if ((e = hipMemcpyAsync(s.d_bytes, s.h_bytes, warm, hipMemcpyHostToDevice, s.stream)) == hipSuccess)
+                e = hipMemcpyAsync(s.h_bytes, s.d_bytes, warm, hipMemcpyDeviceToHost, s.stream);
+        }
+        for (auto& s : c->slot)
+            if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+        if (e != hipSuccess) {
+            fail(c, e, "lvlip_csum_ctx_create (copy engine start)");
+            for (auto& t : c->slot) free_slot(t);
+            delete c;
+            return LVLIP_EHIP;
+        }
+    }
     *out = c;
     return LVLIP_OK;
 }
