@@ -205,8 +205,9 @@ typedef struct lvlip_csum_ctx lvlip_csum_ctx;
  * device arena of `arena_bytes` each (0 = 64 MiB), and its own stream.
  * A context is owned by one thread at a time (src/main.c:83-89 runs the
  * checksum from several threads: give each its own context).  Creation also
- * starts the copy engine (1 MiB each way per slot, LVLIP_WARM_BYTES), so the
- * first call that copies does not pay its start-up (~7 ms).  Returns 0,
+ * starts the copy engine (1 MiB each way per slot, LVLIP_WARM_BYTES) and
+ * loads the kernels' code object, so the first call pays neither start-up
+ * (~7 ms and ~2 ms measured).  Returns 0,
  * LVLIP_ENODEV, LVLIP_ENOMEM (an arena allocation failed) or LVLIP_EHIP. */
 int lvlip_csum_ctx_create(lvlip_csum_ctx **out, int device,
                           size_t arena_bytes);

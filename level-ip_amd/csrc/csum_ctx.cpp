@@ -539,6 +539,8 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         }
         for (auto& s : c->slot)
             if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+        // and the kernels' code object, so the first call launches at once
+        if (e == hipSuccess && lvlip_kernels_load() != 0) e = hipErrorInvalidDeviceFunction;
         if (e != hipSuccess) {
             fail(c, e, "lvlip_csum_ctx_create (copy engine start)");
             for (auto& t : c->slot) free_slot(t);

@@ -457,6 +457,15 @@ const char* lvlip_last_hip_error(void) { return g_last_err; }
 // calling thread.
 void lvlip_set_last_hip_error(const char* msg) { snprintf(g_last_err, sizeof g_last_err, "%s", msg ? msg : ""); }
 
+// Hidden: loads this file's code object on the current device (every product
+// kernel is in it), so a context's first call does not pay the load inside
+// its first launch (~2 ms, measured as the first 64-frame call's time outside
+// its host steps).  Launches nothing.
+int lvlip_kernels_load(void) {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&lvlip::k_window<3, 4>)) == hipSuccess ? 0 : -1;
+}
+
 int lvlip_device_count(void) {
     int c = 0;
     if (hipGetDeviceCount(&c) != hipSuccess) return 0;

@@ -298,6 +298,7 @@ int lvlip_csum_batch_dev_ex(const void*, const lvlip_csum_desc*, uint32_t, uint1
 void lvlip_set_last_hip_error(const char* msg);
 // The host frame calls' device step: mode 0 TX records (u64 per frame), 1 RX
 // header, 2 RX + L4 (u8 verdicts).  Hidden.
+int lvlip_kernels_load(void);  // csum_kernels.hip
 int lvlip_frames_host_launch(int mode, const void* base, const lvlip_frame_desc* frames, uint32_t n,
                              void* out, void* stream);
 }

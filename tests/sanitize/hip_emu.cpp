@@ -92,6 +92,9 @@ int lvlip_csum_batch_dev_ex(const void* base, const lvlip_csum_desc* d, uint32_t
     return LVLIP_OK;
 }
 
+// csum_kernels.hip's code-object load: nothing to load on the CPU
+int lvlip_kernels_load(void) { return 0; }
+
 // The frame calls' device step (csum_kernels.hip lvlip_frames_host_launch):
 // mode 0 TX records, 1 RX header, 2 RX + L4.  Every byte a frame's decisions
 // may read lies inside its descriptor's len, so an overread shows up in ASan.
