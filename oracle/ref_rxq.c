@@ -34,6 +34,7 @@
 #include "skbuff.h"
 
 #include "lvlip_skb.h"
+#include "ref_batch.h"
 
 #define MAX_MARKS 65536
 static const void *g_mark[MAX_MARKS];

@@ -55,6 +55,7 @@
 #include "list.h"
 
 #include "lvlip_skb.h"
+#include "ref_batch.h"
 
 #define ETH_LEN 14 /* include/ethernet.h: struct eth_hdr */
 
@@ -230,14 +231,6 @@ int lvlip_txq_inject(const uint8_t *frame, unsigned int len)
     return 0;
 }
 
-/* What a flush did (lvlip_txq_fill). */
-struct lvlip_txq_report {
-    int frames;  /* frames filled */
-    int rc;      /* the batch call's return: frames, or LVLIP_E* (LVLIP_ENODEV: no context) */
-    int cpu;     /* 1 if the fill fell back to this thread's CPU code after a failure */
-    int dropped; /* malformed frames unlinked and freed, never sent */
-};
-
 /* The flush's fill, as INTEGRATION.md §2a gives it to a maintainer: every
  * queued frame's checksums in ONE call through the context (a queue of at
  * most the context's cpu_max frames is summed on this thread by the library,
@@ -341,6 +334,14 @@ static int fill_held(lvlip_csum_ctx *ctx, struct lvlip_txq_report *r)
     return r->frames = k;
 }
 
+/* The whole flush in one call: lvlip_txq_fill, then lvlip_txq_send.  Returns
+ * the frames sent, or the fill's negative LVLIP_E* (nothing sent). */
+int lvlip_txq_flush(lvlip_csum_ctx *ctx, struct lvlip_txq_report *r)
+{
+    const int rc = lvlip_txq_fill(ctx, r);
+    return rc < 0 ? rc : lvlip_txq_send();
+}
+
 /* skb_reset_header (src/skbuff.c:50-54; weak in oracle/Makefile's copy of
  * skbuff.o): a held frame is flushed, with everything queued before it, before
  * the retransmit rewrites its headers. */
@@ -348,8 +349,8 @@ void skb_reset_header(struct sk_buff *skb)
 {
     if (g_hold && is_held(skb)) {
         struct lvlip_txq_report r;
-        lvlip_txq_fill(g_hold_ctx, &r);
-        g_early_frames += (unsigned long)lvlip_txq_send();
+        const int sent = lvlip_txq_flush(g_hold_ctx, &r);
+        if (sent > 0) g_early_frames += (unsigned long)sent;
     }
     skb->data = skb->end - skb->dlen;
     skb->len = skb->dlen;

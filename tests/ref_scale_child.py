@@ -76,8 +76,12 @@ class SkBuffHead(ctypes.Structure):  # include/skbuff.h:25-29
     _fields_ = [("next", ctypes.c_void_p), ("prev", ctypes.c_void_p), ("qlen", ctypes.c_uint32)]
 
 
-class TxqReport(ctypes.Structure):  # oracle/ref_txq.c: struct lvlip_txq_report
+class TxqReport(ctypes.Structure):  # oracle/ref_batch.h: struct lvlip_txq_report
     _fields_ = [("frames", ctypes.c_int), ("rc", ctypes.c_int), ("cpu", ctypes.c_int), ("dropped", ctypes.c_int)]
+
+
+class BurstReport(ctypes.Structure):  # oracle/ref_batch.h: struct lvlip_rxtxq_report
+    _fields_ = [("rx_cpu", ctypes.c_int), ("queued", ctypes.c_int), ("sent", ctypes.c_int), ("tx", TxqReport)]
 
 
 def burst(n, seed, kinds):
@@ -136,6 +140,8 @@ def main(out_path, so_path, mode, opts_json):
         lib.lvlip_txq_len.restype = ctypes.c_int
         lib.lvlip_txq_frames.argtypes = [ctypes.POINTER(lvlip.Frame), ctypes.c_int]
         lib.lvlip_txq_set_ctx.argtypes = [ctypes.c_void_p]
+        lib.lvlip_rxtxq_burst.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.c_uint32, ctypes.POINTER(BurstReport)]
         if opts.get("hold"):
             assert lib.lvlip_txq_set_hold(1) == 0
         if mode == "batched":
@@ -156,49 +162,48 @@ def main(out_path, so_path, mode, opts_json):
 
     def run_burst(blob, off, ln):
         """One burst: the skbs queued (untimed, netdev_rx_loop's reads), then
-        the stack over them; returns (wall s, CPU s)."""
+        the stack over them, as ONE C call in either form (level-ip as it is:
+        lvlip_rxq_receive_all; batched: lvlip_rxtxq_burst, oracle/ref_rxtxq.c);
+        returns (wall s, CPU s, (verdicts, report) or None)."""
         q = SkBuffHead()
         q.next = q.prev = ctypes.addressof(q)
         n = len(ln)
         assert lib.lvlip_rxq_fill(ctypes.addressof(q), blob.ctypes.data, off.ctypes.data, ln.ctypes.data, n) == n
+        v = np.zeros(n, np.uint8)
+        if mode == "batched":
+            s0 = ctx.stats()
+            br = BurstReport()
+            t0, c0 = time.perf_counter(), time.process_time()
+            m = lib.lvlip_rxtxq_burst(ctx._h, ctypes.addressof(q), flags, v.ctypes.data, n, ctypes.byref(br))
+            wall, cpu = time.perf_counter() - t0, time.process_time() - c0
+            assert m == n, m
+            assert br.sent == br.tx.frames
+            s1 = ctx.stats()
+            r = {"queued": br.queued, "frames": br.tx.frames, "rc": br.tx.rc, "cpu": br.tx.cpu,
+                 "dropped": br.tx.dropped, "rx_cpu_fallback": br.rx_cpu}
+            r.update({k: s1[k] - s0[k] for k in ("gpu_calls", "cpu_calls", "pieces", "h2d_bytes")})
+            return wall, cpu, (v, r)
         t0, c0 = time.perf_counter(), time.process_time()
         if not batched:
             assert lib.lvlip_rxq_receive_all(ctypes.addressof(q)) == n
             return time.perf_counter() - t0, time.process_time() - c0, None
-        v = np.zeros(n, np.uint8)
-        rx_cpu = ctypes.c_int(0)
-        if mode == "batched":
-            m = lib.lvlip_rxq_verify(ctx._h, ctypes.addressof(q), flags, v.ctypes.data, n, ctypes.byref(rx_cpu))
-            assert m == n, m
-        else:
-            import skb_oracle
+        # mode "oracle": the oracle's verdicts and TX fill (the harness's own check on the CPU)
+        import skb_oracle
 
-            # the walker's frame: skb->data .. skb->end (BUFLEN, the read's zero tail)
-            frames = [bytes(blob[int(o):int(o) + int(ln_)]) + bytes(1600 - int(ln_)) for o, ln_ in zip(off, ln)]
-            v[:] = [skb_oracle.rx_verdict(f, flags) for f in frames]
+        # the walker's frame: skb->data .. skb->end (BUFLEN, the read's zero tail)
+        frames = [bytes(blob[int(o):int(o) + int(ln_)]) + bytes(1600 - int(ln_)) for o, ln_ in zip(off, ln)]
+        v[:] = [skb_oracle.rx_verdict(f, flags) for f in frames]
         assert lib.lvlip_rxq_dispatch(ctypes.addressof(q), v.ctypes.data, 1) == n
-        s0 = ctx.stats() if ctx is not None else None
-        rep = TxqReport()
         nq = lib.lvlip_txq_len()
-        if mode == "batched":
-            assert lib.lvlip_txq_fill(ctx._h, ctypes.byref(rep)) >= 0
-        else:
-            import skb_oracle
-
-            arr = (lvlip.Frame * max(nq, 1))()
-            assert lib.lvlip_txq_frames(arr, nq) == nq
-            for k in range(nq):
-                f = bytearray(ctypes.string_at(arr[k].head, arr[k].len))
-                skb_oracle.tx_fill(f)
-                ctypes.memmove(arr[k].head, bytes(f), len(f))
-            rep.frames = nq
-        assert lib.lvlip_txq_send() == rep.frames
+        arr = (lvlip.Frame * max(nq, 1))()
+        assert lib.lvlip_txq_frames(arr, nq) == nq
+        for k in range(nq):
+            f = bytearray(ctypes.string_at(arr[k].head, arr[k].len))
+            skb_oracle.tx_fill(f)
+            ctypes.memmove(arr[k].head, bytes(f), len(f))
+        assert lib.lvlip_txq_send() == nq
         wall, cpu = time.perf_counter() - t0, time.process_time() - c0
-        r = {"queued": nq, "frames": rep.frames, "rc": rep.rc, "cpu": rep.cpu, "dropped": rep.dropped,
-             "rx_cpu_fallback": rx_cpu.value}
-        if s0 is not None:
-            s1 = ctx.stats()
-            r.update({k: s1[k] - s0[k] for k in ("gpu_calls", "cpu_calls", "pieces", "h2d_bytes")})
+        r = {"queued": nq, "frames": nq, "rc": 0, "cpu": 0, "dropped": 0, "rx_cpu_fallback": 0}
         return wall, cpu, (v, r)
 
     out = {}

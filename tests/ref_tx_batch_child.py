@@ -136,6 +136,7 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
         lib.lvlip_txq_queue.restype = ctypes.c_void_p
         lib.lvlip_txq_inject.argtypes = [ctypes.c_char_p, ctypes.c_uint]
         lib.lvlip_txq_set_ctx.argtypes = [ctypes.c_void_p]
+        lib.lvlip_txq_flush.argtypes = [ctypes.c_void_p, ctypes.POINTER(TxqReport)]
         lib.lvlip_txq_early_frames.restype = ctypes.c_ulong
         lib.lvlip_txq_reheld.restype = ctypes.c_ulong
         if opts.get("hold"):
@@ -162,8 +163,21 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
         assert lib.lvlip_txq_frames(arr, n) == n
         return [ctypes.string_at(arr[k].head, arr[k].len) for k in range(n)]
 
+    timed_stats = {}
+
     def flush():
         if not batched:
+            return
+        if timing and mode == "gpu":
+            # the clock is running: ONE C call (fill, then send); the report
+            # and the context's counters are read after the clock stops
+            ctx = context()
+            rep = TxqReport()
+            sent = lib.lvlip_txq_flush(ctx._h if ctx is not None else None, ctypes.byref(rep))
+            if sent < 0:
+                raise SystemExit(f"lvlip_txq_flush: {sent}")
+            reports.append({"frames": rep.frames, "rc": rep.rc, "cpu": rep.cpu, "dropped": rep.dropped})
+            batches.append(sent)
             return
         n = lib.lvlip_txq_len()
         if mode == "gpu":
@@ -231,6 +245,8 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
     addr_buf = ctypes.create_string_buffer(addr, len(addr))
     lib.tcp_v4_connect(sk, ctypes.addressof(addr_buf), 16, 0)
     payload = ((np.arange(write_bytes, dtype=np.uint64) * 7 + 3) & 0xFF).astype(np.uint8).tobytes()
+    if timing and batched and mode == "gpu" and ctxs and ctxs[0] is not None:
+        timed_stats["s0"] = ctxs[0].stats()
     t0, c0 = time.perf_counter(), time.process_time()
     lib.tcp_send(sk, payload, len(payload))
     lib.tcp_send_next(sk, send_next if send_next > 0 else (write_bytes // 536 + 8))
@@ -246,6 +262,9 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
     lib.tcp_send_reset(sk)
     flush()
     t_tcp = (time.perf_counter() - t0, time.process_time() - c0)
+    if "s0" in timed_stats:  # the TCP phase's counters (the flush before the SYN retransmit included)
+        s1 = ctxs[0].stats()
+        reports[-1].update({k: s1[k] - timed_stats["s0"][k] for k in ("gpu_calls", "cpu_calls", "pieces", "h2d_bytes")})
     # echo requests -> icmpv4_reply
     skbs = [make_golden._frame_to_skb(lib, req) for req in requests]
     t0, c0 = time.perf_counter(), time.process_time()
