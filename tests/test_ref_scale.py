@@ -46,6 +46,18 @@ def _check(base, got, n):
     assert got["cpu_header_sums"] == 0 and got["batch_header_sums"] == got["verdicts"].get("1", 0)
 
 
+def _calls(r, n, cpu_max):
+    """(GPU calls, CPU calls) the burst's two library calls should make: the
+    RX verify over n + 1 frames (the ARP request too), then the TX flush over
+    r["queued"] replies, each on the GPU above the threshold (r holds the
+    context's counters over the whole burst)."""
+    import lvlip
+
+    t = lvlip.CPU_MAX_DEFAULT if cpu_max is None else cpu_max
+    gpu = int(n + 1 > t) + int(r["queued"] > t)
+    return gpu, 2 - gpu
+
+
 def test_rx_tx_burst_oracle_composition(tmp_path):
     """CPU: 2 000 frames with the oracle's verdicts and TX fill in place of the
     library (the harness's own check on a machine without a GPU)."""
@@ -62,16 +74,13 @@ def test_rx_tx_burst_at_scale(tmp_path, cpu_max):
     flush of ~11 000 replies stays on the calling thread; with threshold 0
     both run on the GPU.  The tap bytes equal the unbatched stack's, frame for
     frame, and no header is summed on the CPU."""
-    import lvlip
-
     opts = {"n": 30000, "seed": 6, "kinds": "all"}
     base = run(tmp_path, RXQ, "unbatched", opts)
     got = run(tmp_path, RXTXQ, "batched", opts, cpu_max=cpu_max, tag=f"b{cpu_max}")
     _check(base, got, 30000)
     r = got["reports"][0]
     assert r["cpu"] == 0 and r["frames"] == r["queued"] > 5000
-    on_gpu = cpu_max == 0 or r["queued"] > lvlip.CPU_MAX_DEFAULT
-    assert (r["gpu_calls"], r["cpu_calls"]) == ((1, 0) if on_gpu else (0, 1)), r
+    assert (r["gpu_calls"], r["cpu_calls"]) == _calls(r, 30000, cpu_max), r
 
 
 @pytest.mark.gpu
@@ -84,7 +93,7 @@ def test_rx_tx_small_burst_default_threshold_on_cpu(tmp_path):
     got = run(tmp_path, RXTXQ, "batched", opts)
     _check(base, got, 40)
     r = got["reports"][0]
-    assert r["cpu_calls"] == 1 and r["gpu_calls"] == 0
+    assert (r["gpu_calls"], r["cpu_calls"]) == (0, 2)
 
 
 @pytest.mark.skipif(not os.path.exists(RXTXQ_SLAB), reason="oracle/_ref/libref_rxtxq_slab.so not built")
@@ -109,9 +118,10 @@ def test_rx_tx_burst_from_registered_slab(tmp_path):
     got = run(tmp_path, RXTXQ_SLAB, "batched", dict(opts, slab=1 << 28), cpu_max=0, tag="slab_gpu")
     _check(base, got, 30000)
     r = got["reports"][0]
-    assert r["gpu_calls"] == 1 and r["cpu"] == 0 and r["frames"] == r["queued"] > 5000
-    # the queued replies (~800-B frames in 256-B granules) moved as spans, not gathered
-    assert r["h2d_bytes"] < 3 * 1600 * r["queued"], r
+    assert r["gpu_calls"] == 2 and r["cpu"] == 0 and r["frames"] == r["queued"] > 5000
+    # the burst's skbs (1 600-B buffers in 256-B granules) and the queued
+    # replies moved as their own spans, not the whole 256 MiB slab
+    assert r["h2d_bytes"] < 2 * 1792 * (30001 + r["queued"]), r
 
 
 @pytest.mark.gpu
@@ -144,13 +154,10 @@ def test_rx_tx_burst_hold_at_scale(tmp_path, cpu_max):
     """30 000 frames, the replies held by reference: one RX call, the
     dispatch, one lvlip_tx_checksum over the held replies; tap bytes equal
     the unbatched stack's with either threshold."""
-    import lvlip
-
     opts = {"n": 30000, "seed": 12, "kinds": "all", "hold": 1}
     base = run(tmp_path, RXQ, "unbatched", opts)
     got = run(tmp_path, RXTXQ, "batched", opts, cpu_max=cpu_max, tag=f"hold{cpu_max}")
     _check(base, got, 30000)
     r = got["reports"][0]
     assert r["cpu"] == 0 and r["frames"] == r["queued"] > 5000
-    on_gpu = cpu_max == 0 or r["queued"] > lvlip.CPU_MAX_DEFAULT
-    assert (r["gpu_calls"], r["cpu_calls"]) == ((1, 0) if on_gpu else (0, 1)), r
+    assert (r["gpu_calls"], r["cpu_calls"]) == _calls(r, 30000, cpu_max), r
