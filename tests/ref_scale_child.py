@@ -40,7 +40,8 @@ ONE lvlip_tx_checksum, sends them and frees the skbs.
 
 OPTIONS (JSON): {"n": frames in the burst (after one ARP request), "seed",
 "kinds": "all" (every ip_rcv drop reason, tests/ref_rx_cases.py) or "ok" (echo
-requests only), "flags": the RX verify flags, "time": [burst sizes] (tap =
+requests only), "flags": the RX verify flags, "device": the context's device (an
+invalid index: no context, both calls on the CPU), "time": [burst sizes] (tap =
 /dev/null; each size timed after an untimed burst of the same size; the
 context made and warmed first)}.
 
@@ -128,6 +129,7 @@ def main(out_path, so_path, mode, opts_json):
     batched = mode != "unbatched"
     flags = int(opts.get("flags", 0))
     ctx = None
+    out_ctx_error = None
     hist, reports = {}, []
     if batched:
         import lvlip
@@ -145,12 +147,16 @@ def main(out_path, so_path, mode, opts_json):
         if opts.get("hold"):
             assert lib.lvlip_txq_set_hold(1) == 0
         if mode == "batched":
-            ctx = lvlip.Context(0)
-            lib.lvlip_txq_set_ctx(ctx._h)
-            if opts.get("slab"):
+            try:
+                ctx = lvlip.Context(int(opts.get("device", 0)))
+            except lvlip.LvlipError as e:  # no device: both calls fall back to the CPU
+                ctx, out_ctx_error = None, e.rc
+            if ctx is not None:
+                lib.lvlip_txq_set_ctx(ctx._h)
+            if ctx is not None and opts.get("slab"):
                 assert lvlip.lib().lvlip_csum_register(ctx._h, lib.lvlip_slab_base(), int(opts["slab"]),
                                                        lvlip.REG_DMA) == 0
-            if opts.get("time"):  # warm the GPU path (pinned pages, kernel load) before any clock
+            if ctx is not None and opts.get("time"):  # warm the GPU path before any clock
                 import workloads
 
                 cm = ctx.cpu_max
@@ -171,17 +177,19 @@ def main(out_path, so_path, mode, opts_json):
         assert lib.lvlip_rxq_fill(ctypes.addressof(q), blob.ctypes.data, off.ctypes.data, ln.ctypes.data, n) == n
         v = np.zeros(n, np.uint8)
         if mode == "batched":
-            s0 = ctx.stats()
+            s0 = ctx.stats() if ctx is not None else None
             br = BurstReport()
             t0, c0 = time.perf_counter(), time.process_time()
-            m = lib.lvlip_rxtxq_burst(ctx._h, ctypes.addressof(q), flags, v.ctypes.data, n, ctypes.byref(br))
+            m = lib.lvlip_rxtxq_burst(ctx._h if ctx is not None else None, ctypes.addressof(q), flags,
+                                      v.ctypes.data, n, ctypes.byref(br))
             wall, cpu = time.perf_counter() - t0, time.process_time() - c0
             assert m == n, m
             assert br.sent == br.tx.frames
-            s1 = ctx.stats()
             r = {"queued": br.queued, "frames": br.tx.frames, "rc": br.tx.rc, "cpu": br.tx.cpu,
                  "dropped": br.tx.dropped, "rx_cpu_fallback": br.rx_cpu}
-            r.update({k: s1[k] - s0[k] for k in ("gpu_calls", "cpu_calls", "pieces", "h2d_bytes")})
+            if s0 is not None:
+                s1 = ctx.stats()
+                r.update({k: s1[k] - s0[k] for k in ("gpu_calls", "cpu_calls", "pieces", "h2d_bytes")})
             return wall, cpu, (v, r)
         t0, c0 = time.perf_counter(), time.process_time()
         if not batched:
@@ -236,6 +244,8 @@ def main(out_path, so_path, mode, opts_json):
             raise SystemExit("reader did not see the end marker")
     if ctx is not None:
         ctx.close()
+    if out_ctx_error is not None:
+        out["context_error"] = out_ctx_error
     out.update({"frames": got, "verdicts": hist, "reports": reports,
                 "cpu_header_sums": int(lib.lvlip_rxq_computed()), "batch_header_sums": int(lib.lvlip_rxq_skipped())})
     with open(out_path, "w") as f:

@@ -161,3 +161,18 @@ def test_rx_tx_burst_hold_at_scale(tmp_path, cpu_max):
     r = got["reports"][0]
     assert r["cpu"] == 0 and r["frames"] == r["queued"] > 5000
     assert (r["gpu_calls"], r["cpu_calls"]) == _calls(r, 30000, cpu_max), r
+
+
+@pytest.mark.parametrize("hold", [0, 1])
+def test_rx_tx_burst_no_context_runs_on_cpu(tmp_path, hold):
+    """CPU: the batched stack as one C call per burst (lvlip_rxtxq_burst,
+    oracle/ref_rxtxq.c) with no context (an invalid device: LVLIP_ENODEV):
+    the RX verify and the TX fill both fall back to the library's CPU code,
+    and the tap bytes are the unbatched stack's, replies copied or held."""
+    opts = {"n": 2000, "seed": 13, "kinds": "all", "device": 99, "hold": hold}
+    base = run(tmp_path, RXQ, "unbatched", opts)
+    got = run(tmp_path, RXTXQ, "batched", opts, tag=f"nodev{hold}")
+    assert got["context_error"] == -2
+    _check(base, got, 2000)
+    r = got["reports"][0]
+    assert r["rx_cpu_fallback"] == 1 and r["cpu"] == 1 and r["rc"] == -2 and r["frames"] == r["queued"], r
