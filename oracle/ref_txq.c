@@ -82,7 +82,8 @@ int lvlip_txq_set_hold(int on)
     return 0;
 }
 
-/* The context the flush before a retransmit uses (NULL: the CPU fill). */
+/* The context the flush before a retransmit uses (NULL: the CPU fill).  Set
+ * it back to NULL before destroying that context. */
 void lvlip_txq_set_ctx(lvlip_csum_ctx *ctx) { g_hold_ctx = ctx; }
 
 /* frames sent by the flushes skb_reset_header made before rewriting a held skb */

@@ -243,6 +243,7 @@ def main(out_path, so_path, mode, opts_json):
         if th.is_alive():
             raise SystemExit("reader did not see the end marker")
     if ctx is not None:
+        lib.lvlip_txq_set_ctx(None)  # the harness keeps no pointer to a destroyed context
         ctx.close()
     if out_ctx_error is not None:
         out["context_error"] = out_ctx_error

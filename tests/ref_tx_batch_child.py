@@ -279,6 +279,7 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
             raise SystemExit("reader did not see the end marker")
     for c in ctxs:
         if c is not None:
+            lib.lvlip_txq_set_ctx(None)  # the harness keeps no pointer to a destroyed context
             c.close()
     out.update({"frames": got, "batches": batches, "deferred": deferred, "reports": reports})
     if batched:
