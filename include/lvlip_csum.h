@@ -249,7 +249,7 @@ int lvlip_csum_batch_host_flat(lvlip_csum_ctx *ctx, const void *base,
  *                       lvlip_rx_verify (flags 0) needs 74 B of each frame
  *                       and always reads a zero-copy region in place
  * "Densely" means the packets' byte span is at most twice their bytes plus
- * 1 MiB AND they come in address order: the sum of the jumps between
+ * 1 MiB (the factor is LVLIP_SPAN_RATIO, 1-64) AND they come in address order: the sum of the jumps between
  * consecutive start addresses is at most twice the span plus 1 MiB (a
  * shuffled batch over a large slab would cut into pieces of one or two
  * packets, each moving a whole span).  A DMA region's batch that is not dense

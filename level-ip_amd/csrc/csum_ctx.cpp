@@ -466,6 +466,12 @@ int lvlip_csum_ctx_create(lvlip_csum_ctx** out, int device, size_t arena_bytes) 
         const long long v = e ? atoll(e) : 32768;
         c->inline_max = v > 0 ? (uint32_t)(v > 0xffffffffll ? 0xffffffffll : v) : 0u;
     }
+    // LVLIP_SPAN_RATIO (1-64): the density rule's span-to-bytes ratio (span_dense)
+    {
+        const char* e = getenv("LVLIP_SPAN_RATIO");
+        const long long v = e ? atoll(e) : 2;
+        c->span_ratio = (uint32_t)(v < 1 ? 1 : v > 64 ? 64 : v);
+    }
     // LVLIP_CPU_MAX: host calls of at most this many packets / frames run on
     // the calling thread (lvlip_csum_ctx_set_cpu_max; 0: always the GPU)
     {
@@ -687,7 +693,7 @@ int lvlip_csum_batch_host(lvlip_csum_ctx* c, const lvlip_csum_iov* pkts, uint32_
                 }
             });
             const bool inside = !outside.load();
-            if (inside && fd && span_dense(span_merge(part, np)))
+            if (inside && fd && span_dense(span_merge(part, np), c->span_ratio))
                 // refused only when one packet's 16-B span exceeds the arena
                 // (the flat call's rule): then the gather below takes it
                 rc = host_flat_impl(c, r->host, r->bytes, fd, n, out, 1);

@@ -111,6 +111,10 @@ struct lvlip_csum_ctx {
     // other cores and made the composed stack up to 2x costlier per frame
     // ("Where batch-and-dispatch pays")
     uint32_t inline_max = 32768;
+    // LVLIP_SPAN_RATIO: a registered region's items move as spans with the
+    // copy engine when their span is at most this many times their bytes
+    // (plus 1 MiB) and in address order (span_dense)
+    uint32_t span_ratio = 2;
     bool inline_call = false;  // the current call is one of those
     lvlip_ctx::Slot slot[lvlip_ctx::kSlots];
     std::vector<lvlip_ctx::Region> regions;
@@ -168,7 +172,7 @@ inline void trim_scratch(lvlip_csum_ctx* c) {
 
 // Whether items cover their byte span densely AND in call order, the condition
 // for moving whole spans (DMA, or the flat call's span copy): the span at most
-// twice their bytes plus 1 MiB, and the jumps between consecutive start
+// span_ratio (2) times their bytes plus 1 MiB, and the jumps between consecutive start
 // addresses summing to at most twice the span plus 1 MiB.  Pieces are runs in
 // call order cut at the piece size, so a shuffled batch over a large buffer
 // would cut into pieces of one or two items, each moving a whole span (ADVICE
@@ -202,10 +206,17 @@ inline SpanScan span_merge(const SpanScan* p, uint32_t np) {
     }
     return t;
 }
-inline bool span_dense(const SpanScan& s) {
+// ratio: the context's span_ratio (2; LVLIP_SPAN_RATIO).  A span moved by the
+// copy engine costs the link its bytes and the host nothing; a gather costs
+// the host a copy of every item's bytes.  Inside level-ip's stack, replies
+// in a slab's 1 792-B granules (2.2x their bytes) moved as spans (ratio 3)
+// ran 3-6 % faster per frame than gathered at 16K frames and tied at 4K
+// (DESIGN.md §9); for an isolated call the pool's gather keeps the link
+// time at the items' own bytes, so the default stays 2.
+inline bool span_dense(const SpanScan& s, uint32_t ratio) {
     if (!s.any() || s.hi <= s.lo) return false;
     const uint64_t span = s.hi - s.lo;
-    return span <= 2 * s.sum + (1ull << 20) && s.jumps <= 2 * span + (1ull << 20);
+    return span <= (uint64_t)ratio * s.sum + (1ull << 20) && s.jumps <= 2 * span + (1ull << 20);
 }
 
 struct DeviceGuard {
@@ -285,7 +296,7 @@ bool dense_ordered(lvlip_csum_ctx* c, uint32_t n, const Addr& addr_of, const Len
             part[j] = s;
         }
     });
-    return span_dense(span_merge(part, np));
+    return span_dense(span_merge(part, np), c->span_ratio);
 }
 
 }  // namespace lvlip_ctx

@@ -392,7 +392,7 @@ RegionScan scan_region(lvlip_csum_ctx* c, const lvlip_frame* fr, uint32_t n) {
         out.fits = out.fits && fits[j];
     }
     out.r = r;
-    out.dense = out.fits && span_dense(span_merge(part, np));
+    out.dense = out.fits && span_dense(span_merge(part, np), c->span_ratio);
     return out;
 }
 
