@@ -131,6 +131,41 @@ __attribute__((target("avx512f,avx512bw,avx2"))) static uint32_t sum_words_avx51
 }
 #endif
 
+/* Short buffers (IPv4 headers, ICMP/TCP headers alone: under 64 B) without
+ * the vector path's setup and lane reduction: 8-byte loads into two packed
+ * accumulators of two 32-bit fields each (at most 7 steps, so no field
+ * carries), then the last 0-7 bytes.  Same u32 wrap-around sum as the rest. */
+static inline uint32_t sum_words_short(const uint8_t *p, int count)
+{
+    uint64_t a = 0, b = 0;
+    while (count >= 8) {
+        uint64_t x;
+        memcpy(&x, p, 8);
+        a += x & 0x0000ffff0000ffffull;
+        b += (x >> 16) & 0x0000ffff0000ffffull;
+        p += 8;
+        count -= 8;
+    }
+    uint32_t s = (uint32_t)a + (uint32_t)(a >> 32) + (uint32_t)b + (uint32_t)(b >> 32);
+    if (count >= 4) {
+        uint32_t x;
+        memcpy(&x, p, 4);
+        s += (x & 0xffffu) + (x >> 16);
+        p += 4;
+        count -= 4;
+    }
+    if (count >= 2) {
+        uint16_t w;
+        memcpy(&w, p, 2);
+        s += w;
+        p += 2;
+        count -= 2;
+    }
+    if (count > 0) /* utils.c:34-35: left-over byte, zero-extended */
+        s += *p;
+    return s;
+}
+
 typedef uint32_t (*sum_fn)(const uint8_t *, int);
 static sum_fn g_sum; /* chosen once; racing first callers store the same value */
 
@@ -157,22 +192,31 @@ static sum_fn pick_sum(void)
     return f;
 }
 
-/* src/utils.c:22-38 */
-uint32_t sum_every_16bits(void *addr, int count)
+/* sum_every_16bits's body, called directly by checksum (no PLT hop): short
+ * buffers inline, the rest through the path picked for the CPU */
+static inline uint32_t sum16(const uint8_t *p, int count)
 {
     if (count <= 0)
         return 0;
+    if (count < 64)
+        return sum_words_short(p, count);
     sum_fn f = __atomic_load_n(&g_sum, __ATOMIC_RELAXED);
     if (!f)
         f = pick_sum();
-    return f((const uint8_t *)addr, count);
+    return f(p, count);
+}
+
+/* src/utils.c:22-38 */
+uint32_t sum_every_16bits(void *addr, int count)
+{
+    return sum16((const uint8_t *)addr, count);
 }
 
 /* src/utils.c:40-55 */
 uint16_t checksum(void *addr, int count, int start_sum)
 {
     uint32_t sum = (uint32_t)start_sum;
-    sum += sum_every_16bits(addr, count);
+    sum += sum16((const uint8_t *)addr, count);
     sum = (sum & 0xffff) + (sum >> 16); /* <= 0x1fffe */
     sum = (sum & 0xffff) + (sum >> 16); /* <= 0xffff: same as the while loop */
     return (uint16_t)~sum;
