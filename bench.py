@@ -97,6 +97,8 @@ def parse(argv=None):
     p.add_argument("--crossover", action="store_true",
                    help="diag: host calls at n = 1..256K frames on both sides of the CPU/GPU threshold "
                         "(lvlip_csum_ctx_set_cpu_max), wall and CPU time per call")
+    p.add_argument("--no-crossover", action="store_true",
+                   help="with --frames: leave the crossover curve out (kernel traces of the frame calls)")
     p.add_argument("--e2e", action="store_true",
                    help="also time the host-resident path (PCIe-inclusive; stderr + diag)")
     return p.parse_args(argv)
@@ -568,7 +570,7 @@ def run(args, world: int):
             diag["read_probe_GBps"] = read_probe(lvlip, torch, base, stream)
         if args.frames:
             diag["frames_dev"] = frames_dev(lvlip, torch, dev)
-        if args.frames or args.crossover:
+        if (args.frames and not args.no_crossover) or args.crossover:
             diag["crossover"] = crossover(lvlip, dev)
         if args.e2e:
             diag["e2e_host_GBps"] = e2e(lvlip, b, base)
@@ -729,14 +731,21 @@ def echo_reply_timing(lvlip, torch, base, fd, fdt, pay, stream, reps=7):
     echo request (type 8, code 0; its checksum field is whatever the TX fill
     left, so flags 0's field is the RFC 1624 one, not verified), then
     lvlip_icmp_echo_reply_dev with flags 0 (one 64-B sector per frame) and
-    with LVLIP_ECHO_FULL (each lane sums its whole message), HIP events around
-    each launch alone; the request bytes are restored before every launch.
-    GB/s counts the ICMP messages' bytes."""
+    with LVLIP_ECHO_FULL (the flat sweep over the requests' messages), HIP
+    events around each launch alone; the request bytes are restored before
+    every launch.  Everything the call needs is made before the first event,
+    so the pair holds the ctypes call and the kernel only (round 5's form
+    made the status tensor between the events and read ~20 % slower than
+    the kernel trace).  GB/s counts the ICMP messages' bytes."""
     icmp = pay["start_sum"] == 0
     t_off = torch.from_numpy((fd["offset"][icmp] + 34).astype(np.int64)).to(base.device)
     msg_bytes = int(pay["len"][icmp].sum())
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     out = {"icmp_frames": int(icmp.sum()), "icmp_bytes": msg_bytes}
+    lib = lvlip.lib()
+    n = fd.size
+    st = torch.empty(n, dtype=torch.uint8, device=base.device)
+    args = (base.data_ptr(), fdt.data_ptr(), n)
     for name, flags in (("flags0", 0), ("full", lvlip.ECHO_FULL)):
         ms = []
         for _ in range(reps):
@@ -744,9 +753,13 @@ def echo_reply_timing(lvlip, torch, base, fd, fdt, pay, stream, reps=7):
             base[t_off + 1] = 0
             torch.cuda.synchronize()
             e0.record(stream)
-            st = lvlip.icmp_echo_reply_dev(base, fdt, stream=stream, flags=flags)
+            if flags == 0:
+                rc = lib.lvlip_icmp_echo_reply_dev(*args, st.data_ptr(), stream.cuda_stream)
+            else:
+                rc = lib.lvlip_icmp_echo_reply_dev_ex(*args, flags, st.data_ptr(), stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize()
+            assert rc == lvlip.OK, rc
             ms.append(e0.elapsed_time(e1))
         med = sorted(ms)[len(ms) // 2]
         out[name] = {"ms": round(med, 4), "GBps": round(msg_bytes / med / 1e6, 1),
