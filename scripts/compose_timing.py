@@ -53,7 +53,7 @@ def rx(lib, mode, cpu_max=None, slab=0, hold=False, **extra_env):
             return json.load(f)["time"]
 
 
-def tx(lib, mode, w, cpu_max=None, hold=False, **extra_env):
+def tx(lib, mode, w, cpu_max=None, hold=False, slab=0, **extra_env):
     env = env_for(cpu_max)
     env.update({k: str(v) for k, v in extra_env.items()})
     with tempfile.TemporaryDirectory() as d:
@@ -61,7 +61,8 @@ def tx(lib, mode, w, cpu_max=None, hold=False, **extra_env):
         with open(req, "w") as f:
             json.dump([], f)
         subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ref_tx_batch_child.py"), req, out,
-                        os.path.join(REF, lib), mode, json.dumps({"write_bytes": w, "send_next": 0, "time": True, "hold": hold})],
+                        os.path.join(REF, lib), mode, json.dumps({"write_bytes": w, "send_next": 0, "time": True, "hold": hold,
+                                                             "slab": slab})],
                        check=True, stdin=subprocess.DEVNULL, env=env, timeout=900)
         with open(out) as f:
             o = json.load(f)
@@ -98,7 +99,15 @@ def main():
                                    ("batched_cpu", "libref_txq.so", "gpu", 1 << 30, {}),
                                    ("hold_default", "libref_txq.so", "gpu", None, {"hold": True}),
                                    ("hold_gpu", "libref_txq.so", "gpu", 0, {"hold": True}),
-                                   ("hold_cpu", "libref_txq.so", "gpu", 1 << 30, {"hold": True})):
+                                   ("hold_cpu", "libref_txq.so", "gpu", 1 << 30, {"hold": True}),
+                                   # every skb buffer from one registered slab, on both sides
+                                   ("unbatched_slab", "libref_fixclock_slab.so", "unbatched", None,
+                                    {"slab": 1 << 30}),
+                                   ("slab_hold_default", "libref_txq_slab.so", "gpu", None,
+                                    {"hold": True, "slab": 1 << 30}),
+                                   ("slab_hold_gpu", "libref_txq_slab.so", "gpu", 0, {"hold": True, "slab": 1 << 30}),
+                                   ("slab_hold_cpu", "libref_txq_slab.so", "gpu", 1 << 30,
+                                    {"hold": True, "slab": 1 << 30})):
         res["tx"][tag] = {str(w): tx(lib, mode, w, cm, **ex) for w in WRITES}
         print("tx", tag, res["tx"][tag], file=sys.stderr, flush=True)
     print(json.dumps(res))

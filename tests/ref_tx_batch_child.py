@@ -36,6 +36,9 @@ OPTIONS (JSON, all optional):
   device       the context's device (default 0; an invalid index makes
                lvlip_csum_ctx_create fail, so the flush fills on the CPU)
   hashes       report frames as sha1 hex digests instead of their bytes
+  slab         bytes: with oracle/_ref/libref_{txq,fixclock}_slab.so, every
+               skb buffer from one slab (oracle/ref_slab.c), which the batched
+               run's context registers LVLIP_REG_DMA
   hold         the queue holds each skb by reference instead of copying it
                (lvlip_txq_set_hold, oracle/ref_txq.c): the flush fills the
                frame array with ONE lvlip_tx_checksum, and a retransmit
@@ -113,6 +116,10 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
 
         th = threading.Thread(target=reader, daemon=True)
         th.start()
+    if opts.get("slab"):
+        lib.lvlip_slab_init.argtypes = [ctypes.c_size_t]
+        lib.lvlip_slab_base.restype = ctypes.c_void_p
+        assert lib.lvlip_slab_init(int(opts["slab"])) == 0
     lib.netdev_init()
     lib.route_init()
     lib.arp_rcv.argtypes = [ctypes.POINTER(make_golden.SkBuff)]
@@ -152,6 +159,9 @@ def main(req_path: str, out_path: str, so_path: str, mode: str, opts_json: str =
             try:
                 ctxs.append(lvlip.Context(int(opts.get("device", 0))))
                 lib.lvlip_txq_set_ctx(ctxs[0]._h)
+                if opts.get("slab"):
+                    assert lvlip.lib().lvlip_csum_register(ctxs[0]._h, lib.lvlip_slab_base(), int(opts["slab"]),
+                                                           lvlip.REG_DMA) == 0
             except lvlip.LvlipError as e:
                 out["context_error"] = e.rc
                 ctxs.append(None)

@@ -232,3 +232,36 @@ def test_tx_batch_hold_at_scale(tmp_path):
         r = got["reports"][0]
         # the injected failure stops the call at its first piece
         assert r["gpu_calls"] == 1 and r["pieces"] >= (1 if extra else 2) and r["cpu"] == (1 if extra else 0), r
+
+
+TXQ_SLAB = os.path.join(ROOT, "oracle", "_ref", "libref_txq_slab.so")
+FIXCLOCK_SLAB = os.path.join(ROOT, "oracle", "_ref", "libref_fixclock_slab.so")
+SLAB = {"slab": 1 << 28}
+
+
+@pytest.mark.skipif(not (os.path.exists(TXQ_SLAB) and os.path.exists(FIXCLOCK_SLAB)),
+                    reason="oracle/_ref/libref_{txq,fixclock}_slab.so not built")
+def test_tx_batch_slab_hold_oracle(tmp_path):
+    """CPU: every skb buffer from one slab (oracle/ref_slab.c) on both sides,
+    the TX frames held and filled by the oracle: the tap bytes equal the
+    unbatched stack's (with the same slab, and without it)."""
+    base = _run(tmp_path, FIXCLOCK_SLAB, "unbatched", SLAB, tag="unbatched_slab")
+    assert base["frames"] == _run(tmp_path, FIXCLOCK, "unbatched", tag="unbatched_plain")["frames"]
+    _check_same(base, _run(tmp_path, TXQ_SLAB, "oracle", dict(SLAB, hold=True), tag="slab_hold_oracle"))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not (os.path.exists(TXQ_SLAB) and os.path.exists(FIXCLOCK_SLAB)),
+                    reason="oracle/_ref/libref_{txq,fixclock}_slab.so not built")
+def test_tx_batch_slab_hold_at_scale(tmp_path):
+    """The 12 MiB tcp_send with every skb buffer in one registered slab and
+    the frames held: one GPU call moves the write queue's segments as spans
+    (their 768-B granules are dense, in order), tap bytes identical."""
+    base = _run(tmp_path, FIXCLOCK_SLAB, "unbatched", dict(SCALE, **SLAB), tag="unb_slab_scale")
+    n_tcp = 1 + 2 + (SCALE["write_bytes"] + 535) // 536 + 2
+    got = _run(tmp_path, TXQ_SLAB, "gpu", dict(SCALE, hold=True, **SLAB), env=_env(0), tag="slab_hold_scale")
+    _check_same(base, got, first_batch=n_tcp - 1)
+    r = got["reports"][0]
+    assert r["gpu_calls"] == 1 and r["cpu"] == 0, r
+    # spans: about the segments' granules, not a gather of each frame (~604 B)
+    assert 700 * r["frames"] < r["h2d_bytes"] < 1600 * r["frames"], r
