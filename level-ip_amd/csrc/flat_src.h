@@ -248,7 +248,9 @@ __device__ __forceinline__ void fr_store16_pol(uint64_t a, uint32_t c) {
 // field (the request's code is 0: both callers checked it).
 template <int STP>
 __device__ __forceinline__ void fr_store_echo_reply(uint8_t* m, uint32_t field) {
-    if constexpr (STP == 0) {
+    if constexpr (STP == 7) {  // lab timing only: no reply written (wrong bytes)
+        (void)m, (void)field;
+    } else if constexpr (STP == 0) {
         m[0] = 0u;
         m[2] = (uint8_t)field;
         m[3] = (uint8_t)(field >> 8);
@@ -276,7 +278,7 @@ constexpr int kEchoStore = 0;
 template <int MODE, int SEC = 0, int STP = 0>
 struct FrameSrc {
     static_assert(SEC == 0 || SEC == 32 || SEC == 64, "field block size");
-    static_assert(STP == 0 || (STP >= 2 && STP <= 6), "field store policy");
+    static_assert(STP == 0 || (STP >= 2 && STP <= 6) || (MODE == FR_ECHO && STP == 7), "field store policy");
     const uint8_t* base;             // the frames' bytes
     uint8_t* wbase;                  // the same, writable (TX)
     const lvlip_frame_desc* frames;  // this launch's first frame

@@ -695,7 +695,8 @@ __attribute__((visibility("default"))) int lvlip_lab_batch_dev_ex(const void* ba
 // field (k_echo_reply), variant = the reply's store form (fr_store_echo_reply:
 // 0 three byte stores, 2-6 two u16 stores with that cache policy; the
 // patched 16-B window chunk of flags 0 was measured and removed, last in
-// commit 72b8c4f); mode 5 variant 8: byte stores with a three-chunk window
+// commit 72b8c4f); variant 7: no reply store at all (timing only, the
+// frames keep the request's bytes); mode 5 variant 8: byte stores with a three-chunk window
 // (the product's since round 5), variant 0 etc. the four-chunk window.
 __attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int variant, void* base,
                                                                 const lvlip_frame_desc* frames, uint32_t n,
@@ -718,7 +719,7 @@ __attribute__((visibility("default"))) int lvlip_lab_frames_dev(int mode, int va
             return hipGetLastError() == hipSuccess ? LVLIP_OK : LVLIP_EHIP;
         }
         switch (variant) {
-            LVLIP_ECHO(0) LVLIP_ECHO(2) LVLIP_ECHO(3) LVLIP_ECHO(4) LVLIP_ECHO(5) LVLIP_ECHO(6)
+            LVLIP_ECHO(0) LVLIP_ECHO(2) LVLIP_ECHO(3) LVLIP_ECHO(4) LVLIP_ECHO(5) LVLIP_ECHO(6) LVLIP_ECHO(7)
             default: return LVLIP_EINVAL;
         }
 #undef LVLIP_ECHO
