@@ -261,3 +261,58 @@ def test_inline_and_pool_host_steps_agree(inline_max, monkeypatch):
         got = ctx.batch_host(seg, [0] * len(seg))
         ref = np.array([pyoracle.checksum(s or b"\0", len(s), 0) for s in seg], np.uint16)
         assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("ratio", ["2", "3"])
+def test_span_ratio_moves_half_full_granules(ratio, monkeypatch):
+    """LVLIP_SPAN_RATIO: frames each in its own 1 792-B granule of a
+    registered DMA slab (level-ip's RX skbs: BUFLEN 1 600 rounded to 256 B),
+    ~2.2x their bytes.  Ratio 2 (the default) gathers them (h2d bytes about
+    the frames' own); ratio 3 moves the granules as spans (h2d bytes about
+    the slab's).  The fills equal the oracle either way."""
+    monkeypatch.setenv("LVLIP_SPAN_RATIO", ratio)
+    fr = workloads.frames(4096, seed=160, max_l4=1460)
+    fr = [f for f in fr if len(f) <= 1000][:2048]  # at most 1 000 B each, ~530 B on average
+    want = [bytearray(f) for f in fr]
+    for f in want:
+        skb_oracle.tx_fill(f)
+    gran = 1792
+    buf = np.zeros(gran * len(fr) + 64, dtype=np.uint8)
+    views = []
+    for i, f in enumerate(fr):
+        o = i * gran + 14  # skb->data at head + 14: the frame from head
+        buf[o:o + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
+        views.append(buf[o:o + len(f)])
+    frame_bytes = sum(len(f) for f in fr)
+    span = gran * len(fr)
+    assert span > 2 * frame_bytes + (1 << 20) and span < 3 * frame_bytes + (1 << 20)
+    with lvlip.Context(0, cpu_max=0) as ctx:
+        ctx.register(buf, lvlip.REG_DMA)
+        try:
+            s0 = ctx.stats()
+            ctx.tx_checksum(views)
+            moved = ctx.stats()["h2d_bytes"] - s0["h2d_bytes"]
+        finally:
+            ctx.unregister(buf)
+    assert [bytes(v) for v in views] == [bytes(w) for w in want]
+    if ratio == "2":
+        assert moved < 1.3 * frame_bytes, (moved, frame_bytes)
+    else:
+        assert 0.9 * span < moved < 1.1 * span, (moved, span)
+
+
+@pytest.mark.parametrize("warm", ["0", "1048576"])
+def test_context_without_and_with_copy_engine_warmup(warm, monkeypatch):
+    """LVLIP_WARM_BYTES: a context made with no copy-engine warm-up (0) and
+    with the default's; a call of several pieces (the later ones through the
+    copy engine) fills the frames as the oracle does either way."""
+    monkeypatch.setenv("LVLIP_WARM_BYTES", warm)
+    fr = workloads.frames(6000, seed=170, max_l4=1460)
+    want = [bytearray(f) for f in fr]
+    for f in want:
+        skb_oracle.tx_fill(f)
+    got = [bytearray(f) for f in fr]
+    with lvlip.Context(0, arena_bytes=1 << 20, cpu_max=0) as ctx:
+        ctx.tx_checksum(got)
+        assert ctx.stats()["pieces"] >= 3
+    assert [bytes(f) for f in got] == [bytes(w) for w in want]
